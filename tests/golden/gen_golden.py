@@ -1,0 +1,494 @@
+#!/usr/bin/env python3
+"""Generate the golden input/output vectors under tests/golden/ from the reference.
+
+TEST INFRASTRUCTURE ONLY.  This script imports the reference implementation
+(josef-w/Differentiable-iLQR, mounted read-only at /root/reference) in the BUILD
+container and writes small .npz fixtures (inputs + the reference's outputs).
+It never runs on the GPU box; only the .npz files travel.  Nothing from the
+reference is copied: the fixtures are data.
+
+Recipes follow SURVEY.md §8(c):
+  * flat imports with PYTHONDONTWRITEBYTECODE (the tree is read-only);
+  * rocket.py does `from casadi import *` only for its animation code
+    (rocket.py:6, 959, 1006) -> an empty stand-in module named `casadi`;
+  * the Riccati sweep is reached through the LQRStepFn.forward closure;
+  * the DiLQR implicit backward is driven through LQRStep(no_op_forward=True)
+    (backward through mpc_explicit.MPC itself raises under torch 2.10);
+  * data/*.pkl are NOT unpickled: their opcode stream is parsed statically
+    with pickletools and only the embedded tensor storages are loaded, with
+    torch.load(weights_only=True).
+
+Usage:  python tests/golden/gen_golden.py   (takes ~1-2 minutes on 8 cores)
+"""
+import contextlib
+import io
+import os
+import pickletools
+import sys
+import types
+
+sys.dont_write_bytecode = True
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def _import_reference():
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    sys.modules.setdefault("casadi", types.ModuleType("casadi"))
+    import util
+    import pnqp
+    import mpc            # before lqr_step: mpc.py <-> lqr_step.py import each other
+    import lqr_step
+    import mpc_backup     # likewise for lqr_step_backup.py
+    import lqr_step_backup
+    import lqr_step_explicit
+    import mpc_explicit
+    from env_dx import cartpole, pendulum, rocket
+    return types.SimpleNamespace(
+        util=util, pnqp=pnqp, lqr_step_explicit=lqr_step_explicit, lqr_step_backup=lqr_step_backup,
+        lqr_step=lqr_step, mpc_explicit=mpc_explicit, mpc=mpc,
+        cartpole=cartpole, pendulum=pendulum, rocket=rocket)
+
+
+R = _import_reference()
+
+
+@contextlib.contextmanager
+def default_dtype(dt):
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dt)
+    try:
+        yield
+    finally:
+        torch.set_default_dtype(old)
+
+
+def np_(t):
+    if isinstance(t, (list, tuple)):
+        return np.stack([np_(x) for x in t])
+    if isinstance(t, torch.Tensor):
+        return t.detach().cpu().numpy()
+    return np.asarray(t)
+
+
+def save(name, **arrs):
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
+    print(f"  wrote {name}.npz ({os.path.getsize(path)/1024:.1f} KiB)")
+
+
+def model(name):
+    return {"pendulum": R.pendulum.PendulumDx, "cartpole": R.cartpole.CartpoleDx,
+            "rocket": R.rocket.RocketDx}[name]()
+
+
+def tname(dt):
+    return "f64" if dt == torch.float64 else "f32"
+
+
+# --------------------------------------------------------------------------
+# random inputs (numpy RandomState so the oracle tests can regenerate them)
+# --------------------------------------------------------------------------
+def sample_states(name, N, rng, wide=True):
+    if name == "pendulum":
+        th = rng.uniform(-np.pi, np.pi, N)
+        dth = rng.uniform(-8, 8, N)
+        x = np.stack([np.cos(th), np.sin(th), dth], 1)
+        u = rng.uniform(-3, 3, (N, 1))       # beyond the +-2 clamp
+    elif name == "cartpole":
+        th = rng.uniform(-np.pi, np.pi, N)
+        x = np.stack([rng.uniform(-1, 1, N), rng.uniform(-2, 2, N), np.cos(th), np.sin(th),
+                      rng.uniform(-3, 3, N)], 1)
+        u = rng.uniform(-150, 150, (N, 1)) if wide else rng.uniform(-5, 5, (N, 1))
+    elif name == "rocket":
+        r = rng.uniform([0, -4, -2.5], [10, 4, 2.5], (N, 3))
+        v = rng.normal(0, 1.0, (N, 3))
+        q = np.array([1., 0, 0, 0]) + 0.3 * rng.normal(size=(N, 4))
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+        w = rng.normal(0, 0.5, (N, 3))
+        x = np.concatenate([r, v, q, w], 1)
+        u = rng.uniform(-30, 30, (N, 3))
+    return x, u
+
+
+def random_lqr(n, m, T, B, rng):
+    """SURVEY.md §8(d) Riccati workload: C=LL^T+0.1I, c~N, F=[I+0.05N | 0.1N]."""
+    d = n + m
+    L = rng.normal(size=(T, B, d, d)) * 0.5 / np.sqrt(d)
+    C = L @ np.swapaxes(L, -1, -2) + 0.1 * np.eye(d)
+    c = rng.normal(size=(T, B, d))
+    F = np.concatenate([np.eye(n) + 0.05 * rng.normal(size=(T - 1, B, n, n)),
+                        0.1 * rng.normal(size=(T - 1, B, n, m))], -1)
+    f = 0.1 * rng.normal(size=(T - 1, B, n))
+    return C, c, F, f
+
+
+def riccati_closure(step_mod, n, m, T, **kw):
+    fn = step_mod.LQRStep(n, m, T, **kw).__self__.forward
+    cells = dict(zip(fn.__code__.co_freevars, [c.cell_contents for c in fn.__closure__]))
+    return cells["lqr_backward"]
+
+
+# --------------------------------------------------------------------------
+# A. dynamics models: forward, get_linear_dyn, get_matrices, grad_input
+# --------------------------------------------------------------------------
+def case_models():
+    print("A. models")
+    for dt in (torch.float64, torch.float32):
+        with default_dtype(dt):
+            out = {}
+            for name in ("pendulum", "cartpole", "rocket"):
+                rng = np.random.RandomState(100)
+                N = 64
+                x, u = sample_states(name, N, rng)
+                dx = model(name)
+                X, U = torch.tensor(x, dtype=dt), torch.tensor(u, dtype=dt)
+                with torch.no_grad():
+                    out[f"{name}_x"] = x
+                    out[f"{name}_u"] = u
+                    out[f"{name}_fwd"] = np_(dx(X, U))
+                    out[f"{name}_D"] = np_(dx.get_linear_dyn(X, U))
+                    Ns = 16
+                    mats = dx.get_matrices(X[:Ns], U[:Ns])
+                    for k, v in zip(("D", "D_params", "D_x", "D_u", "x_theta", "x_xtm1", "x_utm1"), mats):
+                        out[f"{name}_gm_{k}"] = np_(v)
+                    # grad_input over a short random closed-loop trajectory
+                    T, B = 6, 3
+                    rng2 = np.random.RandomState(7)
+                    xs, us = sample_states(name, T * B, rng2, wide=False)
+                    Xs = torch.tensor(xs.reshape(T, B, -1), dtype=dt)
+                    Us = torch.tensor(us.reshape(T, B, -1), dtype=dt)
+                    K = torch.tensor(rng2.normal(size=(T, B, dx.n_ctrl, dx.n_state)) * 0.3, dtype=dt)
+                    gi = dx.grad_input(Xs, Us, K)
+                    out[f"{name}_gi_X"], out[f"{name}_gi_U"], out[f"{name}_gi_K"] = np_(Xs), np_(Us), np_(K)
+                    for k, v in zip(("grad_D", "grad_d", "D_x", "D_u", "D", "d_x", "d_u"), gi):
+                        out[f"{name}_gi_{k}"] = np_(v)
+            save(f"models_{tname(dt)}", **out)
+
+
+# --------------------------------------------------------------------------
+# B. Riccati sweep (lqr_backward) unconstrained / bounded / Cholesky variant
+# --------------------------------------------------------------------------
+def case_riccati():
+    print("B. riccati")
+    shapes = {"pendulum": (3, 1, 10, 16), "cartpole": (5, 1, 25, 16), "rocket": (13, 3, 30, 8)}
+    for dt in (torch.float64, torch.float32):
+        with default_dtype(dt):
+            out = {}
+            for name, (n, m, T, B) in shapes.items():
+                rng = np.random.RandomState(0)
+                C, c, F, _ = random_lqr(n, m, T, B, rng)
+                u = rng.uniform(-0.5, 0.5, (T, B, m))
+                Ct, ct, Ft, ut = (torch.tensor(a, dtype=dt) for a in (C, c, F, u))
+                out[f"{name}_C"], out[f"{name}_c"], out[f"{name}_F"], out[f"{name}_u"] = C, c, F, u
+                ctx = types.SimpleNamespace(current_u=ut)
+                with torch.no_grad():
+                    lb = riccati_closure(R.lqr_step_explicit, n, m, T)
+                    Ks, ks, _ = lb(ctx, Ct, ct, Ft, None)
+                    out[f"{name}_K"], out[f"{name}_k"] = np_(Ks[::-1]), np_(ks[::-1])
+                    lo, hi = -1.0, 1.0
+                    lb = riccati_closure(R.lqr_step_explicit, n, m, T, u_lower=lo, u_upper=hi)
+                    Ks, ks, nqp = lb(ctx, Ct, ct, Ft, None)
+                    out[f"{name}_box_K"], out[f"{name}_box_k"] = np_(Ks[::-1]), np_(ks[::-1])
+                    out[f"{name}_box_nqp"] = np.array(nqp)
+                    # adjoint engine (lqr_step_backup: Cholesky + 1e-6 I for m>1)
+                    lb = riccati_closure(R.lqr_step_backup, n, m, T)
+                    Ks, ks, _ = lb(ctx, Ct, ct, Ft, None)
+                    out[f"{name}_chol_K"], out[f"{name}_chol_k"] = np_(Ks[::-1]), np_(ks[::-1])
+                    # u_zero_I branch (active-set masked solve used by the adjoints)
+                    I = torch.tensor(rng.uniform(size=(T, B, m)) < 0.3)
+                    lb = riccati_closure(R.lqr_step_backup, n, m, T, u_zero_I=I)
+                    Ks, ks, _ = lb(ctx, Ct, ct, Ft, None)
+                    out[f"{name}_zI"] = np_(I)
+                    out[f"{name}_zI_K"], out[f"{name}_zI_k"] = np_(Ks[::-1]), np_(ks[::-1])
+            save(f"riccati_{tname(dt)}", **out)
+
+
+# --------------------------------------------------------------------------
+# C. pnqp box QP
+# --------------------------------------------------------------------------
+def case_pnqp():
+    print("C. pnqp")
+    for dt in (torch.float64, torch.float32):
+        with default_dtype(dt):
+            out = {}
+            for m in (1, 3):
+                rng = np.random.RandomState(3 + m)
+                B = 64
+                L = rng.normal(size=(B, m, m))
+                H = L @ np.swapaxes(L, 1, 2) + 0.2 * np.eye(m)
+                q = rng.normal(size=(B, m)) * 3
+                lo = -rng.uniform(0.1, 1.5, (B, m))
+                hi = rng.uniform(0.1, 1.5, (B, m))
+                x0 = rng.uniform(-2, 2, (B, m))
+                Ht, qt, lot, hit, x0t = (torch.tensor(a, dtype=dt) for a in (H, q, lo, hi, x0))
+                out.update({f"m{m}_H": H, f"m{m}_q": q, f"m{m}_lo": lo, f"m{m}_hi": hi, f"m{m}_x0": x0})
+                with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+                    x, _, If, it = R.pnqp.pnqp(Ht, qt, lot, hit)
+                    out[f"m{m}_x"], out[f"m{m}_If"], out[f"m{m}_it"] = np_(x), np_(If), np.array(it)
+                    x, _, If, it = R.pnqp.pnqp(Ht, qt, -0.7, 0.7, x_init=x0t)
+                    out[f"m{m}_xf"], out[f"m{m}_Iff"], out[f"m{m}_itf"] = np_(x), np_(If), np.array(it)
+                    # per-problem calls (batch size 1): the reference semantics without batch coupling
+                    xs, its = [], []
+                    for b in range(B):
+                        x, _, If, it = R.pnqp.pnqp(Ht[b:b+1], qt[b:b+1], lot[b:b+1], hit[b:b+1])
+                        xs.append(np_(x)[0]); its.append(it)
+                    out[f"m{m}_x_pp"], out[f"m{m}_it_pp"] = np.stack(xs), np.array(its)
+            save(f"pnqp_{tname(dt)}", **out)
+
+
+# --------------------------------------------------------------------------
+# helpers for the solver-level cases
+# --------------------------------------------------------------------------
+def xinit_for(name, B, rng):
+    if name == "pendulum":       # il_env.py:63-66
+        th = rng.uniform(-np.pi / 2, np.pi / 2, B)
+        return np.stack([np.cos(th), np.sin(th), rng.uniform(-1, 1, B)], 1)
+    if name == "cartpole":       # il_env.py:71-75 without the *0
+        th = rng.uniform(-np.pi, np.pi, B)
+        return np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                         rng.uniform(-1, 1, B)], 1)
+    if name == "rocket":         # near hover
+        r = rng.uniform([0, -4, -2.5], [10, 4, 2.5], (B, 3))
+        v = rng.normal(0, 0.1, (B, 3))
+        q = np.array([1., 0, 0, 0]) + 0.05 * rng.normal(size=(B, 4))
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+        w = rng.normal(0, 0.02, (B, 3))
+        return np.concatenate([r, v, q, w], 1)
+
+
+def true_cost(dx, T, B, dt):
+    q, p = dx.get_true_obj()       # il_env.py:159-162 materialisation
+    Q = torch.diag(q).to(dt).unsqueeze(0).unsqueeze(0).repeat(T, B, 1, 1)
+    P = p.to(dt).unsqueeze(0).repeat(T, B, 1)
+    return Q, P
+
+
+# --------------------------------------------------------------------------
+# D. one LQRStep (explicit) forward: Riccati + rollout/line search
+# --------------------------------------------------------------------------
+def case_lqrstep():
+    print("D. lqr step")
+    for dt in (torch.float64, torch.float32):
+        with default_dtype(dt):
+            out = {}
+            for tag, bounds in (("unc", None), ("box", (-5.0, 5.0))):
+                dx = model("cartpole")
+                T, B = 25, 16
+                rng = np.random.RandomState(11)
+                x0 = xinit_for("cartpole", B, rng)
+                u = rng.uniform(-2, 2, (T, B, 1))
+                X0, U = torch.tensor(x0, dtype=dt), torch.tensor(u, dtype=dt)
+                Q, P = true_cost(dx, T, B, dt)
+                mpc_ = R.mpc_explicit.MPC(5, 1, T, lqr_iter=1)
+                with torch.no_grad():
+                    X = R.util.get_traj(T, U, x_init=X0, dynamics=dx)
+                    F, f = mpc_.linearize_dynamics(X, U, dx, diff=False)
+                    kw = {} if bounds is None else dict(u_lower=bounds[0], u_upper=bounds[1])
+                    step = R.lqr_step_explicit.LQRStep(
+                        5, 1, T, true_cost=R.mpc_explicit.QuadCost(Q, P), true_dynamics=dx,
+                        current_x=X, current_u=U, linesearch_decay=0.5, max_linesearch_iter=2, **kw)
+                    nx, nu, nqp, costs, du, malpha = step(X0, Q, P, F, f, None)
+                out.update({f"{tag}_x0": x0, f"{tag}_u": u, f"{tag}_x": np_(X), f"{tag}_F": np_(F),
+                            f"{tag}_f": np_(f), f"{tag}_nx": np_(nx), f"{tag}_nu": np_(nu),
+                            f"{tag}_costs": np_(costs), f"{tag}_du": np_(du), f"{tag}_malpha": np_(malpha),
+                            f"{tag}_nqp": np_(nqp)})
+            save(f"lqrstep_{tname(dt)}", **out)
+
+
+# --------------------------------------------------------------------------
+# E. full MPC (mpc_explicit) solves
+# --------------------------------------------------------------------------
+MPC_CASES = {
+    # name: (model, T, B, lqr_iter, bounds, eps, not_improved_lim, decay, max_ls)
+    "cart_unc": ("cartpole", 25, 16, 10, None, 0.0, 10 ** 9, 0.5, 2),
+    "cart_box10": ("cartpole", 25, 16, 10, (-10.0, 10.0), 0.0, 10 ** 9, 0.5, 2),
+    "cart_il": ("cartpole", 25, 16, 40, (-100.0, 100.0), 1e-4, 5, 0.5, 2),
+    "pend_unc": ("pendulum", 10, 16, 10, None, 0.0, 10 ** 9, 0.2, 5),
+    "pend_box": ("pendulum", 10, 16, 10, (-2.0, 2.0), 0.0, 10 ** 9, 0.2, 5),
+    "rocket_unc": ("rocket", 30, 4, 5, None, 0.0, 10 ** 9, 0.2, 5),
+}
+
+
+def run_mpc(name, dt, lqr_iter_override=None):
+    mname, T, B, it, bounds, eps, nil, decay, mls = MPC_CASES[name]
+    dx = model(mname)
+    rng = np.random.RandomState(0)
+    x0 = xinit_for(mname, B, rng)
+    X0 = torch.tensor(x0, dtype=dt)
+    Q, P = true_cost(dx, T, B, dt)
+    kw = {} if bounds is None else dict(u_lower=bounds[0], u_upper=bounds[1])
+    m = R.mpc_explicit.MPC(dx.n_state, dx.n_ctrl, T, lqr_iter=lqr_iter_override or it, eps=eps,
+                           not_improved_lim=nil, linesearch_decay=decay, max_linesearch_iter=mls,
+                           exit_unconverged=False, detach_unconverged=False, verbose=-1,
+                           grad_method=R.mpc_explicit.GradMethods.ANALYTIC, **kw)
+    with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+        x, u, costs = m(X0, R.mpc_explicit.QuadCost(Q, P), dx)
+    return x0, np_(x), np_(u), np_(costs)
+
+
+def case_mpc():
+    print("E. mpc")
+    for dt in (torch.float64, torch.float32):
+        with default_dtype(dt):
+            out = {}
+            for name in MPC_CASES:
+                x0, x, u, costs = run_mpc(name, dt)
+                out.update({f"{name}_x0": x0, f"{name}_x": x, f"{name}_u": u, f"{name}_costs": costs})
+                if name in ("cart_unc", "cart_box10"):
+                    for k in (1, 2, 3):
+                        _, x, u, costs = run_mpc(name, dt, lqr_iter_override=k)
+                        out.update({f"{name}_it{k}_x": x, f"{name}_it{k}_u": u, f"{name}_it{k}_costs": costs})
+            save(f"mpc_{tname(dt)}", **out)
+
+
+# --------------------------------------------------------------------------
+# F. classic differentiable LQR (mpc.py + lqr_step.py backward)
+# --------------------------------------------------------------------------
+def case_classic_adjoint():
+    print("F. classic adjoint")
+    dt = torch.float64
+    with default_dtype(dt):
+        out = {}
+        for tag, (n, m, T, B, bounds) in {"m1": (5, 1, 10, 3, None), "m3": (4, 3, 8, 3, None),
+                                            "m1box": (5, 1, 10, 3, (-0.5, 0.5)),
+                                            "m3box": (4, 3, 8, 3, (-0.5, 0.5))}.items():
+            rng = np.random.RandomState(21)
+            C, c, F, f = random_lqr(n, m, T, B, rng)
+            x0 = rng.normal(size=(B, n))
+            wx, wu = rng.normal(size=(T, B, n)), rng.normal(size=(T, B, m))
+            Ct, ct, Ft, ft, x0t = (torch.tensor(a, dtype=dt, requires_grad=True) for a in (C, c, F, f, x0))
+            kw = {} if bounds is None else dict(u_lower=bounds[0], u_upper=bounds[1])
+            mpc_ = R.mpc.MPC(n, m, T, lqr_iter=1, n_batch=B, detach_unconverged=False,
+                             exit_unconverged=False, verbose=-1, **kw)
+            with contextlib.redirect_stdout(io.StringIO()):
+                x, u, _ = mpc_(x0t, R.mpc.QuadCost(Ct, ct), R.mpc.LinDx(Ft, ft))
+                loss = (x * torch.tensor(wx)).sum() + (u * torch.tensor(wu)).sum()
+                loss.backward()
+            out.update({f"{tag}_C": C, f"{tag}_c": c, f"{tag}_F": F, f"{tag}_f": f, f"{tag}_x0": x0,
+                        f"{tag}_wx": wx, f"{tag}_wu": wu, f"{tag}_x": np_(x), f"{tag}_u": np_(u),
+                        f"{tag}_dx0": np_(x0t.grad), f"{tag}_dC": np_(Ct.grad), f"{tag}_dc": np_(ct.grad),
+                        f"{tag}_dF": np_(Ft.grad), f"{tag}_df": np_(ft.grad)})
+        save("adjoint_f64", **out)
+
+
+# --------------------------------------------------------------------------
+# G. DiLQR implicit backward (lqr_step_explicit.py:653-712)
+# --------------------------------------------------------------------------
+def implicit_once(mname, T, B, bounds, x, u, x0, Q, P, wx, wu, dt):
+    dx = model(mname)
+    theta = dx.params.detach().clone().to(dt).requires_grad_(True)
+    Qg, Pg = Q.clone().requires_grad_(True), P.clone().requires_grad_(True)
+    m = R.mpc_explicit.MPC(dx.n_state, dx.n_ctrl, T, grad_method=R.mpc_explicit.GradMethods.ANALYTIC)
+    X, U = torch.tensor(x, dtype=dt), torch.tensor(u, dtype=dt)
+    F, f = m.linearize_dynamics(X, U, dx, diff=True)
+    F, f = F.detach(), f.detach()
+    kw = {} if bounds is None else dict(u_lower=bounds[0], u_upper=bounds[1])
+    step = R.lqr_step_explicit.LQRStep(
+        dx.n_state, dx.n_ctrl, T, true_cost=R.mpc_explicit.QuadCost(Qg, Pg), true_dynamics=dx,
+        current_x=X, current_u=U, back_eps=m.back_eps, no_op_forward=True, **kw)
+    with contextlib.redirect_stdout(io.StringIO()):
+        x2, u2 = step(torch.tensor(x0, dtype=dt), Qg, Pg, F, f, theta)
+        loss = (x2 * torch.tensor(wx, dtype=dt)).sum() + (u2 * torch.tensor(wu, dtype=dt)).sum()
+        loss.backward()
+    return np_(Qg.grad), np_(Pg.grad), np_(theta.grad), np_(F), np_(f)
+
+
+def case_implicit():
+    print("G. implicit backward")
+    cases = {"cart_unc": ("cartpole", 10, 4, None, "cart_unc"),
+             "cart_box": ("cartpole", 10, 4, (-5.0, 5.0), "cart_box10"),
+             "pend_box": ("pendulum", 10, 4, (-2.0, 2.0), "pend_box")}
+    for dt in (torch.float64, torch.float32):
+        with default_dtype(dt):
+            out = {}
+            for tag, (mname, T, B, bounds, mpc_case) in cases.items():
+                dx = model(mname)
+                rng = np.random.RandomState(5)
+                x0 = xinit_for(mname, B, rng)
+                Q, P = true_cost(dx, T, B, dt)
+                kw = {} if bounds is None else dict(u_lower=bounds[0], u_upper=bounds[1])
+                _, _, _, _, _, _, _, decay, mls = MPC_CASES[mpc_case]
+                m = R.mpc_explicit.MPC(dx.n_state, dx.n_ctrl, T, lqr_iter=30, eps=1e-6,
+                                       linesearch_decay=decay, max_linesearch_iter=mls,
+                                       exit_unconverged=False, detach_unconverged=False, verbose=-1,
+                                       grad_method=R.mpc_explicit.GradMethods.ANALYTIC, **kw)
+                with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+                    x, u, _ = m(torch.tensor(x0, dtype=dt), R.mpc_explicit.QuadCost(Q, P), dx)
+                x, u = np_(x), np_(u)
+                wx = rng.normal(size=x.shape)
+                wu = rng.normal(size=u.shape)
+                dQ, dP, dth, F, f = implicit_once(mname, T, B, bounds, x, u, x0, Q, P, wx, wu, dt)
+                # per-problem d theta: weight only problem j
+                dth_b = []
+                for j in range(B):
+                    mx, mu = np.zeros_like(wx), np.zeros_like(wu)
+                    mx[:, j], mu[:, j] = wx[:, j], wu[:, j]
+                    dth_b.append(implicit_once(mname, T, B, bounds, x, u, x0, Q, P, mx, mu, dt)[2])
+                out.update({f"{tag}_x0": x0, f"{tag}_x": x, f"{tag}_u": u, f"{tag}_Q": np_(Q),
+                            f"{tag}_P": np_(P), f"{tag}_wx": wx, f"{tag}_wu": wu, f"{tag}_F": F,
+                            f"{tag}_f": f, f"{tag}_dQ": dQ, f"{tag}_dP": dP, f"{tag}_dtheta": dth,
+                            f"{tag}_dtheta_b": np.stack(dth_b)})
+            save(f"implicit_{tname(dt)}", **out)
+
+
+# --------------------------------------------------------------------------
+# H. the reference's own known-answer datasets (data/*.pkl), parsed statically
+# --------------------------------------------------------------------------
+def parse_dataset(path):
+    data = open(path, "rb").read()
+    ops = list(pickletools.genops(data))
+    scalars, tensors = {}, {}
+    last_key = None
+    for i, (op, arg, _pos) in enumerate(ops):
+        if op.name in ("SHORT_BINUNICODE", "BINUNICODE") and isinstance(arg, str):
+            last_key = arg
+        elif op.name in ("BININT1", "BININT2", "BININT", "BINFLOAT") and last_key is not None:
+            scalars.setdefault(last_key, arg)
+            last_key = None
+        elif op.name == "BINBYTES":
+            storage = torch.load(io.BytesIO(arg), weights_only=True)
+            flat = torch.tensor(storage.tolist(), dtype=storage.dtype)
+            # following ops: offset, size tuple, stride tuple (torch._utils._rebuild_tensor_v2)
+            ints = []
+            for op2, arg2, _ in ops[i + 1:i + 40]:
+                if op2.name in ("BININT1", "BININT2", "BININT"):
+                    ints.append(arg2)
+                if op2.name in ("NEWTRUE", "NEWFALSE"):
+                    break
+            off, rest = ints[0], ints[1:]
+            nd = len(rest) // 2
+            size, stride = rest[:nd], rest[nd:]
+            owner = [k for k in ("params", "goal_state", "goal_weights", "train_data", "val_data",
+                                 "test_data") if k not in tensors][0]
+            tensors[owner] = torch.as_strided(flat, size, stride, off).clone().numpy()
+    return scalars, tensors
+
+
+def case_datasets():
+    print("H. datasets")
+    out = {}
+    for env in ("cartpole", "pendulum"):
+        scalars, tensors = parse_dataset(os.path.join(REF, "data", env + ".pkl"))
+        for k in ("train_data", "val_data", "test_data", "params"):
+            out[f"{env}_{k}"] = tensors[k]
+        for k in ("lqr_iter", "mpc_T", "linesearch_decay", "max_linesearch_iter", "mpc_eps", "lower", "upper"):
+            out[f"{env}_{k}"] = np.array(scalars[k])
+    save("datasets", **out)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["models", "riccati", "pnqp", "lqrstep", "mpc", "adjoint", "implicit",
+                             "datasets"]
+    table = {"models": case_models, "riccati": case_riccati, "pnqp": case_pnqp,
+             "lqrstep": case_lqrstep, "mpc": case_mpc, "adjoint": case_classic_adjoint,
+             "implicit": case_implicit, "datasets": case_datasets}
+    for w in which:
+        table[w]()
