@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Headline benchmark: iLQR iterations/s on cartpole T=25, 65536 problems per GPU.
+
+BASELINE.json metric: "iLQR iters/sec (whole node), batch=65536 cartpole T=25 at
+1/2/4/8 MI355X" (configs[1]; configs[4] = the same at 8 GPUs, sharded).
+
+A step = one iLQR iteration of mpc_explicit.MPC.forward (mpc_explicit.py:246-299)
+over the rank's 65536 problems: rollout-linearise-Riccati-line search (one fused
+kernel) + best-iterate/stop bookkeeping.  Steps run as whole solves from u = 0
+(lqr_iter = 10 per solve, the MPC default; the initial rollout of each solve is
+inside the timed region).  eps = 0 and not_improved_lim = inf keep every
+iteration live (the reference's own fixed-iteration protocol).
+
+Multi-GPU: one process per GPU (torchrun); problems shard as contiguous slices
+of the one generated set; no collective in the data path (weak scaling).  The
+barrier + synchronize bracket the timed region; the time is the MAX over ranks.
+
+Prints ONE JSON line on rank 0 with `roofline` (fused iteration kernel, HIP
+events on its stream) and `cpu_baseline` (the numpy oracle, a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "differentiable-ilqr_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+T_HORIZON = 25
+B_PER_GPU = 65536
+N_STATE, N_CTRL = 5, 1
+D = N_STATE + N_CTRL
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# Algorithmic bytes, fp32:
+#  fused iteration, per problem: C, c, x_init, tau in / tau out, cost, du_norm
+ITER_BYTES_PER_PROBLEM = 4 * (T_HORIZON * D * D + T_HORIZON * D + N_STATE + 2 * T_HORIZON * D + 2)   # 5,428
+#  Riccati sweep, per problem: C, c_back, F in; K, k out
+SWEEP_BYTES_PER_PROBLEM = 4 * (T_HORIZON * D * D + T_HORIZON * D + (T_HORIZON - 1) * N_STATE * D
+                               + T_HORIZON * N_CTRL * N_STATE + T_HORIZON * N_CTRL)                  # 7,680
+
+
+def make_problems(B_total, seed=0):
+    """x,dx ~ U(-.5,.5), th ~ U(-pi,pi), dth ~ U(-1,1)."""
+    rng = np.random.RandomState(seed)
+    th = rng.uniform(-np.pi, np.pi, B_total)
+    x0 = np.stack([rng.uniform(-.5, .5, B_total), rng.uniform(-.5, .5, B_total), np.cos(th), np.sin(th),
+                   rng.uniform(-1, 1, B_total)], 1).astype(np.float32)
+    q = np.array([0.1, 0.1, 1., 1., 0.1, 0.001], np.float32)       # cartpole get_true_obj
+    p = np.array([0., 0., -1., 0., 0., 0.], np.float32)
+    return x0, q, p
+
+
+def shard_rows(B_total, world, rank):
+    per = B_total // world
+    return rank * per, (rank + 1) * per
+
+
+def cpu_baseline(budget_s=12.0, sample=2048):
+    """The numpy oracle ("port") on a bounded sample, single thread."""
+    from oracle import models as om
+    from oracle import mpc as ompc
+    x0, q, p = make_problems(sample, seed=1)
+    x0 = x0.astype(np.float64)
+    C, c = ompc.expand_cost(np.diag(q).astype(np.float64), p.astype(np.float64), T_HORIZON, sample)
+    iters = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        ompc.mpc_forward(om.Cartpole, x0, C, c, T_HORIZON, lqr_iter=2, eps=0.0, not_improved_lim=10 ** 9,
+                         linesearch_decay=0.5, max_linesearch_iter=2)
+        iters += 2
+    dt = time.perf_counter() - t0
+    return {"value": sample * iters / dt, "unit": "problem-iters/s", "cores": 1, "kind": "port",
+            "sample": f"numpy oracle (oracle/mpc.py), cartpole T=25, {sample} problems x {iters} iterations "
+                      f"in {dt:.1f}s, fp64, 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--lqr-iter", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=B_PER_GPU, help="problems per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from dilqr import _native as N
+    from dilqr import ops
+
+    B = args.batch
+    B_total = B * world
+    x0_all, q, p = make_problems(B_total)
+    lo, hi = shard_rows(B_total, world, rank)
+    x0 = torch.tensor(x0_all[lo:hi], device=dev)
+    C = torch.diag(torch.tensor(q)).repeat(T_HORIZON, B, 1, 1).to(dev).contiguous()     # materialised per (t,b)
+    c = torch.tensor(p).repeat(T_HORIZON, B, 1).to(dev).contiguous()
+    theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
+    ws = ops.MPCWorkspace(T_HORIZON, B, N_STATE, N_CTRL, dev)
+    bounds, _ = N.make_bounds(None, None)
+    stream = torch.cuda.current_stream(dev)
+    s = N.stream(dev)
+
+    def start_solve():
+        ws.ua.zero_()
+        ws.ctrl.zero_()
+        N.call("dilqr_rollout_f32", N.MODEL_CARTPOLE, N_STATE, N_CTRL, T_HORIZON, B, N.ptr(theta), None, None,
+               N.ptr(x0), N.ptr(ws.ua), N.ptr(ws.xa), s)
+
+    state = {"i": 0}
+
+    def step():
+        if state["i"] % args.lqr_iter == 0:
+            start_solve()
+        ops.ilqr_iterate(N.MODEL_CARTPOLE, theta, x0, C, c, ws, bounds, 0.5, 2, state["i"] % args.lqr_iter == 0,
+                         1e-4, 0.0, 10 ** 9)
+        state["i"] += 1
+
+    for _ in range(args.warmup):
+        step()
+    state["i"] = 0
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    assert bool(torch.isfinite(ws.best_cost).all()), "non-finite costs"
+
+    # ---- roofline of the dominant kernel: the fused iteration, timed with
+    # events on ITS stream (the current stream, where ops launch it)
+    reps = 10
+    start_solve()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for r in range(reps):
+        ev[r][0].record(stream)
+        N.call("dilqr_ilqr_iterate_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C),
+               N.ptr(c), N.ptr(ws.xa), N.ptr(ws.ua), bounds, 0.5, 2, N.ptr(ws.ws), N.ptr(ws.xb), N.ptr(ws.ub),
+               N.ptr(ws.cost), N.ptr(ws.du_sq), N.ptr(ws.alpha), None, s)
+        ev[r][1].record(stream)
+        ws.xa, ws.xb = ws.xb, ws.xa
+        ws.ua, ws.ub = ws.ub, ws.ua
+    torch.cuda.synchronize(dev)
+    iter_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    iter_bytes = ITER_BYTES_PER_PROBLEM * B
+
+    # standalone Riccati sweep (the north-star's >=50% HBM target kernel)
+    F, _f = ops.linearize(N.MODEL_CARTPOLE, theta, ws.xa, ws.ua)
+    K = torch.empty(T_HORIZON, B, N_CTRL, N_STATE, device=dev)
+    k = torch.empty(T_HORIZON, B, N_CTRL, device=dev)
+    cb = torch.randn(T_HORIZON, B, D, device=dev)
+    nb = N.Bounds(N.BOUNDS_NONE, 0.0, 0.0, None, None)
+    sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for r in range(reps):
+        sev[r][0].record(stream)
+        N.call("dilqr_lqr_backward_f32", N_STATE, N_CTRL, T_HORIZON, B, N.ptr(C), N.ptr(cb), None, None, N.ptr(F),
+               nb, None, 0, N.ptr(K), N.ptr(k), None, s)
+        sev[r][1].record(stream)
+    torch.cuda.synchronize(dev)
+    sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in sev]))
+    sweep_bytes = SWEEP_BYTES_PER_PROBLEM * B
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("k_ilqr_iterate_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        value = B_total * args.steps / elapsed
+        achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
+        sweep_gbs = sweep_bytes / (sweep_ms * 1e-3) / 1e9
+        line = {
+            "metric": "iLQR iters/sec (whole node), batch=65536 cartpole T=25 at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "problem-iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SURVEY.md §8(d) config 2 x_init, seed 0; cartpole get_true_obj cost materialised "
+                    "per (t,b))",
+            "config": {"workload": "cartpole n=5 m=1 T=25, unconstrained iLQR, 65536 problems per GPU, "
+                                   f"whole-batch solves of lqr_iter={args.lqr_iter} from u=0",
+                       "batch_per_gpu": B, "global_batch": B_total, "T": T_HORIZON,
+                       "parallelism": f"batch-sharded x{world} (no collective)",
+                       "batch_iters_per_s": world * args.steps / elapsed},
+            "roofline": {"kernel": "k_ilqr_iterate<Cartpole> (fused linearise+Riccati+line search)",
+                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": iter_bytes, "avg_launch_ms": iter_ms},
+            "riccati_roofline": {"kernel": "k_lqr_backward<5,1,UNC> (standalone sweep, F from HBM)",
+                                 "bound": "hbm", "achieved": sweep_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": sweep_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": sweep_bytes,
+                                 "avg_launch_ms": sweep_ms},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,521 @@
+// dilqr_device.h — device building blocks of the batched iLQR hot path (gfx950).
+//
+// Mapping: ONE PROBLEM PER LANE ("thread per problem", TPP).  The per-step
+// matrices of a problem are tiny (cartpole: C 6x6, F 5x6, V 5x5), so a lane
+// keeps its problem's V, v, Q, gains and trajectory state in VGPRs with every
+// index a compile-time constant (all loops fully unrolled), and a wave runs 64
+// independent problems in lock-step with no cross-lane traffic at all.  Each
+// lane's per-step record in HBM ([T,B,...] time-major, as the reference lays it
+// out) is contiguous, and the 64 records a wave touches at step t are adjacent,
+// so a wave's loads of one step stream one contiguous span of HBM.
+//
+// Everything here restates the reference math (file:line cited per routine);
+// only the batch mapping differs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dilqr.h"
+
+#define DEV __device__ __forceinline__
+
+namespace dilqr {
+
+// ------------------------------------------------------------------ loads/stores
+// Vectorised load/store of one lane's contiguous record of K floats.  Record
+// offsets are multiples of K floats and the base is 16-byte aligned (checked on
+// the host), so K%4==0 -> dwordx4, K%2==0 -> dwordx2.
+template <int K>
+DEV void ld(float (&r)[K], const float* __restrict__ p) {
+  if constexpr (K % 4 == 0) {
+    const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+    for (int i = 0; i < K / 4; ++i) {
+      float4 v = q[i];
+      r[4 * i] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
+    }
+  } else if constexpr (K % 2 == 0) {
+    const float2* q = reinterpret_cast<const float2*>(p);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+      float2 v = q[i];
+      r[2 * i] = v.x; r[2 * i + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < K; ++i) r[i] = p[i];
+  }
+}
+
+template <int K>
+DEV void st(float* __restrict__ p, const float (&r)[K]) {
+  if constexpr (K % 4 == 0) {
+    float4* q = reinterpret_cast<float4*>(p);
+#pragma unroll
+    for (int i = 0; i < K / 4; ++i) q[i] = make_float4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+  } else if constexpr (K % 2 == 0) {
+    float2* q = reinterpret_cast<float2*>(p);
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) q[i] = make_float2(r[2 * i], r[2 * i + 1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < K; ++i) p[i] = r[i];
+  }
+}
+
+template <int R, int Cc>
+DEV void ld2(float (&r)[R][Cc], const float* __restrict__ p) {
+  ld<R * Cc>(*reinterpret_cast<float(*)[R * Cc]>(&r[0][0]), p);
+}
+template <int R, int Cc>
+DEV void st2(float* __restrict__ p, const float (&r)[R][Cc]) {
+  st<R * Cc>(p, *reinterpret_cast<const float(*)[R * Cc]>(&r[0][0]));
+}
+
+// ------------------------------------------------------------------ bounds
+struct Bounds {
+  int mode;
+  float lo, hi;
+  const float* __restrict__ lo_t;
+  const float* __restrict__ hi_t;
+};
+
+// util.eclamp (util.py:58-72): x<lo -> lo, x>hi -> hi, written exactly (the
+// equality tests of pnqp.py:32 depend on it).  NaN stays NaN.
+DEV float eclamp(float x, float lo, float hi) {
+  x = (x < lo) ? lo : x;
+  x = (x > hi) ? hi : x;
+  return x;
+}
+
+// ------------------------------------------------------------------ small solves
+// Gaussian elimination with partial pivoting for an MxM system with R right-hand
+// sides, everything in registers (M<=4).  Used for Q_uu^{-1} (pinverse of a
+// nonsingular matrix), pnqp's masked LU (pnqp.py:53-54) and lu_solve of the
+// free block (lqr_step_explicit.py:150).
+template <int M, int R>
+DEV void gauss_solve(float (&A)[M][M], float (&X)[M][R]) {
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    // pivot search (compile-time indexed conditional swaps keep data in VGPRs)
+    int p = k;
+    float best = fabsf(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < M; ++i) {
+      float a = fabsf(A[i][k]);
+      if (a > best) { best = a; p = i; }
+    }
+#pragma unroll
+    for (int i = k + 1; i < M; ++i) {
+      if (p == i) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) { float t = A[k][j]; A[k][j] = A[i][j]; A[i][j] = t; }
+#pragma unroll
+        for (int j = 0; j < R; ++j) { float t = X[k][j]; X[k][j] = X[i][j]; X[i][j] = t; }
+      }
+    }
+    float inv = 1.0f / A[k][k];
+#pragma unroll
+    for (int i = k + 1; i < M; ++i) {
+      float l = A[i][k] * inv;
+#pragma unroll
+      for (int j = k + 1; j < M; ++j) A[i][j] -= l * A[k][j];
+#pragma unroll
+      for (int j = 0; j < R; ++j) X[i][j] -= l * X[k][j];
+    }
+  }
+#pragma unroll
+  for (int k = M - 1; k >= 0; --k) {
+    float inv = 1.0f / A[k][k];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      float s = X[k][j];
+#pragma unroll
+      for (int i = k + 1; i < M; ++i) s -= A[k][i] * X[i][j];
+      X[k][j] = s * inv;
+    }
+  }
+}
+
+// Cholesky solve (A + 0 already regularised by the caller), lqr_step_backup.py:202-204.
+template <int M, int R>
+DEV void chol_solve(const float (&A)[M][M], float (&X)[M][R]) {
+  float L[M][M];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int j = 0; j < M; ++j) L[i][j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    float s = A[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
+    float d = sqrtf(s);
+    L[j][j] = d;
+    float inv = 1.0f / d;
+#pragma unroll
+    for (int i = j + 1; i < M; ++i) {
+      float t = A[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
+      L[i][j] = t * inv;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float y[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      float s = X[i][r];
+#pragma unroll
+      for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+      y[i] = s / L[i][i];
+    }
+#pragma unroll
+    for (int i = M - 1; i >= 0; --i) {
+      float s = y[i];
+#pragma unroll
+      for (int k = i + 1; k < M; ++k) s -= L[k][i] * X[k][r];
+      X[i][r] = s / L[i][i];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ pnqp
+// Projected-Newton box QP  min 1/2 x^T H x + q^T x, lb <= x <= ub, pnqp.py:5-82,
+// evaluated for ONE problem (the reference's semantics at batch size 1).
+// Returns the iteration index at exit (pnqp.py:59 / 82); writes x, the free
+// mask If and the masked matrix H_ (whose inverse gives the gains).
+template <int M>
+DEV int pnqp(const float (&H)[M][M], const float (&q)[M], const float (&lb)[M],
+             const float (&ub)[M], bool have_init, float (&x)[M], float (&If)[M],
+             float (&Hf)[M][M]) {
+  const float GAMMA = 0.1f;
+  if (!have_init) {                                     // pnqp.py:14-19
+    if constexpr (M == 1) {
+      x[0] = -(1.0f / H[0][0]) * q[0];
+    } else {
+      float A[M][M], X[M][1];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) A[i][j] = H[i][j];
+        X[i][0] = q[i];
+      }
+      gauss_solve<M, 1>(A, X);
+#pragma unroll
+      for (int i = 0; i < M; ++i) x[i] = -X[i][0];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) x[i] = eclamp(x[i], lb[i], ub[i]);
+
+  auto obj = [&](const float (&z)[M]) {
+    // 0.5*bquad(z,H) + bdot(q,z)  (pnqp.py:11-12, util.py:50-56)
+    float quad = 0.f;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      float r = 0.f;
+#pragma unroll
+      for (int i = 0; i < M; ++i) r += z[i] * H[i][j];
+      quad += r * z[j];
+    }
+    float lin = 0.f;
+#pragma unroll
+    for (int i = 0; i < M; ++i) lin += q[i] * z[i];
+    return 0.5f * quad + lin;
+  };
+
+  int it = 0;
+  for (it = 0; it < 20; ++it) {                         // pnqp.py:28-78
+    float g[M], g_[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < M; ++j) s += H[i][j] * x[j];
+      g[i] = s + q[i];
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      bool clamped = (x[i] == lb[i] && g[i] > 0.f) || (x[i] == ub[i] && g[i] < 0.f);
+      If[i] = clamped ? 0.f : 1.f;
+      g_[i] = clamped ? 0.f : g[i];
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = 0; j < M; ++j)
+        Hf[i][j] = ((If[i] * If[j]) != 0.f ? H[i][j] : 0.f) + (i == j ? 1e-11f : 0.f);
+    float dx[M];
+    if constexpr (M == 1) {
+      dx[0] = -(1.0f / Hf[0][0]) * g_[0];
+    } else {
+      float A[M][M], X[M][1];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) A[i][j] = Hf[i][j];
+        X[i][0] = g_[i];
+      }
+      gauss_solve<M, 1>(A, X);
+#pragma unroll
+      for (int i = 0; i < M; ++i) dx[i] = -X[i][0];
+    }
+    float nrm = 0.f;
+#pragma unroll
+    for (int i = 0; i < M; ++i) nrm += dx[i] * dx[i];
+    if (!(sqrtf(nrm) >= 1e-4f)) return it;              // pnqp.py:56-59 (per problem)
+
+    float alpha = 1.f;
+    float ox = obj(x);
+    float maybe[M];
+    int count = 0;
+    float max_armijo = GAMMA;
+    while (max_armijo <= GAMMA && count < 10) {         // pnqp.py:65-76
+#pragma unroll
+      for (int i = 0; i < M; ++i) maybe[i] = eclamp(x[i] + alpha * dx[i], lb[i], ub[i]);
+      float den = 0.f;
+#pragma unroll
+      for (int i = 0; i < M; ++i) den += g[i] * (x[i] - maybe[i]);
+      float armijo = (ox - obj(maybe)) / den;
+      if (armijo <= GAMMA) alpha *= 0.1f;
+      max_armijo = armijo;
+      ++count;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) x[i] = maybe[i];
+  }
+  return 19;                                            // pnqp.py:80-82 (i after the loop)
+}
+
+// ------------------------------------------------------------------ Riccati step
+// One step of lqr_backward (lqr_step_explicit.py:63-160) for one problem.
+//   in : C_t [D][D], cb_t [D] (= C_t tau_t + c_t), F_t [N][D] (zero for t = T-1,
+//        which makes Q = C exactly), V/v of step t+1 (zero at t = T-1)
+//   out: K_t [M][N], k_t [M]; V/v of step t.
+enum GainMode { GAIN_UNC = 0, GAIN_CHOL = 1, GAIN_ZERO_I = 2, GAIN_BOX = 3 };
+
+template <int N, int M>
+struct RiccatiState {
+  static constexpr int D = N + M;
+  float V[N][N];
+  float v[N];
+  float prev_k[M];     // pnqp warm start (lqr_step_explicit.py:137-143)
+  bool have_prev;
+  int n_qp;
+
+  DEV void init() {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      v[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) V[i][j] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) prev_k[i] = 0.f;
+    have_prev = false;
+    n_qp = 0;
+  }
+
+  // mode GAIN_ZERO_I uses zI[M] (1 = active); GAIN_BOX uses lb/ub [M] (already
+  // lower-u_t / upper-u_t, lqr_step_explicit.py:132-133).
+  template <int MODE>
+  DEV void step(const float (&C)[D][D], const float (&cb)[D], const float (&F)[N][D],
+                const float (&zI)[M], const float (&lb)[M], const float (&ub)[M],
+                float (&K)[M][N], float (&k)[M]) {
+    // Q = C + (F^T V) F,  q = cb + F^T v   (lqr_step_explicit.py:68-72)
+    float P[D][N];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int kk = 0; kk < N; ++kk) {
+        float s = 0.f;
+#pragma unroll
+        for (int l = 0; l < N; ++l) s += F[l][i] * V[l][kk];
+        P[i][kk] = s;
+      }
+    float Q[D][D], q[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < N; ++kk) s += P[i][kk] * F[kk][j];
+        Q[i][j] = C[i][j] + s;
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int l = 0; l < N; ++l) s += F[l][i] * v[l];
+      q[i] = cb[i] + s;
+    }
+    // partitions (lqr_step_explicit.py:78-83)
+    float Quu[M][M], qu[M];
+#pragma unroll
+    for (int a = 0; a < M; ++a) {
+      qu[a] = q[N + a];
+#pragma unroll
+      for (int b = 0; b < M; ++b) Quu[a][b] = Q[N + a][N + b];
+    }
+
+    if constexpr (MODE == GAIN_UNC && M == 1) {          // lqr_step_explicit.py:86-88
+      float r = 1.0f / Quu[0][0];
+#pragma unroll
+      for (int j = 0; j < N; ++j) K[0][j] = -(r * Q[N][j]);
+      k[0] = -(r * qu[0]);
+    } else if constexpr (MODE == GAIN_UNC || MODE == GAIN_CHOL) {
+      // pinverse (90-96) / cholesky(Q_uu + 1e-6 I) (lqr_step_backup.py:199-208)
+      float A[M][M], X[M][N + 1];
+#pragma unroll
+      for (int a = 0; a < M; ++a) {
+#pragma unroll
+        for (int b = 0; b < M; ++b) A[a][b] = Quu[a][b] + ((MODE == GAIN_CHOL && a == b) ? 1e-6f : 0.f);
+#pragma unroll
+        for (int j = 0; j < N; ++j) X[a][j] = Q[N + a][j];
+        X[a][N] = qu[a];
+      }
+      if constexpr (MODE == GAIN_CHOL) chol_solve<M, N + 1>(A, X);
+      else gauss_solve<M, N + 1>(A, X);
+#pragma unroll
+      for (int a = 0; a < M; ++a) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) K[a][j] = -X[a][j];
+        k[a] = -X[a][N];
+      }
+    } else if constexpr (MODE == GAIN_ZERO_I) {          // lqr_step_backup.py:210-232
+      float A[M][M], X[M][N + 1];
+#pragma unroll
+      for (int a = 0; a < M; ++a) {
+        bool Ia = zI[a] != 0.f;
+#pragma unroll
+        for (int b = 0; b < M; ++b) {
+          bool free_ab = (zI[a] == 0.f) && (zI[b] == 0.f);
+          A[a][b] = (free_ab ? Quu[a][b] : 0.f) + ((a == b && Ia) ? 1e-8f : 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) X[a][j] = Ia ? 0.f : Q[N + a][j];
+        X[a][N] = Ia ? 0.f : qu[a];
+      }
+      if constexpr (M == 1) {
+        float r = 1.0f / A[0][0];
+#pragma unroll
+        for (int j = 0; j < N; ++j) K[0][j] = -(r * X[0][j]);
+        k[0] = -((1.0f / Quu[0][0]) * X[0][N]);          // note: the UNMASKED Q_uu (124-125)
+      } else {
+        gauss_solve<M, N + 1>(A, X);
+#pragma unroll
+        for (int a = 0; a < M; ++a) {
+#pragma unroll
+          for (int j = 0; j < N; ++j) K[a][j] = -X[a][j];
+          k[a] = -X[a][N];
+        }
+      }
+    } else {                                             // GAIN_BOX: pnqp (130-150)
+      float x[M], If[M], Hf[M][M];
+#pragma unroll
+      for (int a = 0; a < M; ++a) x[a] = prev_k[a];
+      int it = pnqp<M>(Quu, qu, lb, ub, have_prev, x, If, Hf);
+      n_qp += 1 + it;
+#pragma unroll
+      for (int a = 0; a < M; ++a) { k[a] = x[a]; prev_k[a] = x[a]; }
+      have_prev = true;
+      if constexpr (M == 1) {
+        float r = 1.0f / Hf[0][0];
+#pragma unroll
+        for (int j = 0; j < N; ++j) K[0][j] = -(r * (If[0] != 0.f ? Q[N][j] : 0.f));
+      } else {
+        float X[M][N];
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+          for (int j = 0; j < N; ++j) X[a][j] = If[a] != 0.f ? Q[N + a][j] : 0.f;
+        gauss_solve<M, N>(Hf, X);
+#pragma unroll
+        for (int a = 0; a < M; ++a)
+#pragma unroll
+          for (int j = 0; j < N; ++j) K[a][j] = -X[a][j];
+      }
+    }
+
+    // V = Qxx + Qxu K + K^T Qux + (K^T Quu) K ; v = qx + Qxu k + K^T qu + (K^T Quu) k
+    // (lqr_step_explicit.py:157-160)
+    float KtQuu[N][M];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int b = 0; b < M; ++b) {
+        float s = 0.f;
+#pragma unroll
+        for (int a = 0; a < M; ++a) s += K[a][i] * Quu[a][b];
+        KtQuu[i][b] = s;
+      }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int a = 0; a < M; ++a) {
+          s1 += Q[i][N + a] * K[a][j];
+          s2 += K[a][i] * Q[N + a][j];
+          s3 += KtQuu[i][a] * K[a][j];
+        }
+        V[i][j] = ((Q[i][j] + s1) + s2) + s3;
+      }
+      float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+      for (int a = 0; a < M; ++a) {
+        s1 += Q[i][N + a] * k[a];
+        s2 += K[a][i] * qu[a];
+        s3 += KtQuu[i][a] * k[a];
+      }
+      v[i] = ((q[i] + s1) + s2) + s3;
+    }
+  }
+};
+
+// 0.5*bquad(tau, C) + bdot(tau, c)  (util.py:130-153 / lqr_step_explicit.py:234);
+// also returns C tau (for c_back = C tau + c).
+template <int D>
+DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D],
+                    float (&Ctau)[D]) {
+  // bquad = (tau^T C) tau
+  float quad = 0.f;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; ++i) r += tau[i] * C[i][j];
+    quad += r * tau[j];
+  }
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < D; ++j) s += C[i][j] * tau[j];
+    Ctau[i] = s;
+  }
+  float lin = 0.f;
+#pragma unroll
+  for (int i = 0; i < D; ++i) lin += tau[i] * c[i];
+  return 0.5f * quad + lin;
+}
+
+template <int D>
+DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D]) {
+  float quad = 0.f;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; ++i) r += tau[i] * C[i][j];
+    quad += r * tau[j];
+  }
+  float lin = 0.f;
+#pragma unroll
+  for (int i = 0; i < D; ++i) lin += tau[i] * c[i];
+  return 0.5f * quad + lin;
+}
+
+}  // namespace dilqr

@@ -1,0 +1,925 @@
+// dilqr_kernels.hip — HIP kernels + C-ABI of the batched differentiable iLQR
+// hot path, gfx950.  See include/dilqr.h for the contract and DESIGN.md for the
+// data layout / roofline of each kernel.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "dilqr_device.h"
+#include "dilqr_models.h"
+
+namespace dilqr {
+
+constexpr int kBlock = 64;   // one wave per workgroup: 64 problems, 4 workgroups per CU
+                             // at B=65536, freely distributed over the 8 XCDs.
+
+static inline int grid_for(long long n) { return (int)((n + kBlock - 1) / kBlock); }
+
+DEV float bound_lo(const Bounds& bd, long long idx) { return bd.mode == DILQR_BOUNDS_TENSOR ? bd.lo_t[idx] : bd.lo; }
+DEV float bound_hi(const Bounds& bd, long long idx) { return bd.mode == DILQR_BOUNDS_TENSOR ? bd.hi_t[idx] : bd.hi; }
+
+// ============================================================ model kernels
+template <class Model>
+__global__ void __launch_bounds__(kBlock) k_dynamics(int N, const float* __restrict__ theta,
+                                                     const float* __restrict__ x, const float* __restrict__ u,
+                                                     float* __restrict__ out) {
+  constexpr int n = Model::N, m = Model::M;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  Model md; md.load(theta);
+  float xi[n], ui[m], o[n];
+  ld(xi, x + (size_t)i * n); ld(ui, u + (size_t)i * m);
+  md.forward(xi, ui, o);
+  st(out + (size_t)i * n, o);
+}
+
+template <class Model>
+__global__ void __launch_bounds__(kBlock) k_linear_dyn(int N, const float* __restrict__ theta,
+                                                       const float* __restrict__ x, const float* __restrict__ u,
+                                                       float* __restrict__ Dout) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  Model md; md.load(theta);
+  float xi[n], ui[m], D[n][d];
+  ld(xi, x + (size_t)i * n); ld(ui, u + (size_t)i * m);
+  md.jacobian(xi, ui, D);
+  st2(Dout + (size_t)i * n * d, D);
+}
+
+// util.get_traj (util.py:104-127)
+template <class Model>
+__global__ void __launch_bounds__(kBlock) k_rollout(int T, int B, const float* __restrict__ theta,
+                                                    const float* __restrict__ x_init, const float* __restrict__ u,
+                                                    float* __restrict__ x_out) {
+  constexpr int n = Model::N, m = Model::M;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Model md; md.load(theta);
+  float xt[n];
+  ld(xt, x_init + (size_t)b * n);
+  st(x_out + (size_t)b * n, xt);
+  for (int t = 0; t < T - 1; ++t) {
+    float ut[m], xn[n];
+    ld(ut, u + ((size_t)t * B + b) * m);
+    md.forward(xt, ut, xn);
+#pragma unroll
+    for (int i = 0; i < n; ++i) xt[i] = xn[i];
+    st(x_out + ((size_t)(t + 1) * B + b) * n, xt);
+  }
+}
+
+// LinDx rollout: x_{t+1} = F_t [x_t;u_t] + f_t
+template <int n, int m>
+__global__ void __launch_bounds__(kBlock) k_rollout_lin(int T, int B, const float* __restrict__ F,
+                                                        const float* __restrict__ f, const float* __restrict__ x_init,
+                                                        const float* __restrict__ u, float* __restrict__ x_out) {
+  constexpr int d = n + m;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float xt[n];
+  ld(xt, x_init + (size_t)b * n);
+  st(x_out + (size_t)b * n, xt);
+  for (int t = 0; t < T - 1; ++t) {
+    size_t tb = (size_t)t * B + b;
+    float ut[m], Ft[n][d], xn[n];
+    ld(ut, u + tb * m); ld2(Ft, F + tb * n * d);
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < n; ++j) s += Ft[i][j] * xt[j];
+#pragma unroll
+      for (int j = 0; j < m; ++j) s += Ft[i][n + j] * ut[j];
+      xn[i] = s;
+    }
+    if (f) {
+      float ft[n]; ld(ft, f + tb * n);
+#pragma unroll
+      for (int i = 0; i < n; ++i) xn[i] += ft[i];
+    }
+#pragma unroll
+    for (int i = 0; i < n; ++i) xt[i] = xn[i];
+    st(x_out + ((size_t)(t + 1) * B + b) * n, xt);
+  }
+}
+
+// MPC.linearize_dynamics ANALYTIC (mpc_explicit.py:516-546)
+template <class Model>
+__global__ void __launch_bounds__(kBlock) k_linearize(int T, int B, const float* __restrict__ theta,
+                                                      const float* __restrict__ x, const float* __restrict__ u,
+                                                      float* __restrict__ F, float* __restrict__ f) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)(T - 1) * B) return;
+  Model md; md.load(theta);
+  float xi[n], ui[m], D[n][d], xn[n], fo[n];
+  ld(xi, x + (size_t)i * n); ld(ui, u + (size_t)i * m);
+  md.forward(xi, ui, xn);
+  md.jacobian(xi, ui, D);
+#pragma unroll
+  for (int r = 0; r < n; ++r) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < n; ++j) s += D[r][j] * xi[j];
+#pragma unroll
+    for (int j = 0; j < m; ++j) s += D[r][n + j] * ui[j];
+    fo[r] = xn[r] - s;
+  }
+  st2(F + (size_t)i * n * d, D);
+  st(f + (size_t)i * n, fo);
+}
+
+// ============================================================ Riccati sweep
+// lqr_backward (lqr_step_explicit.py:54-162) with the delta-space c_back of
+// 630-636 fused.  F [T-1,B,n,d] is read from HBM.
+template <int n, int m, int MODE>
+__global__ void __launch_bounds__(kBlock) k_lqr_backward(int T, int B, const float* __restrict__ C,
+                                                         const float* __restrict__ c, const float* __restrict__ x,
+                                                         const float* __restrict__ u, const float* __restrict__ F,
+                                                         Bounds bd, const unsigned char* __restrict__ zI,
+                                                         float* __restrict__ K, float* __restrict__ k,
+                                                         int* __restrict__ n_qp) {
+  constexpr int d = n + m;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  RiccatiState<n, m> rs;
+  rs.init();
+  for (int t = T - 1; t >= 0; --t) {
+    size_t tb = (size_t)t * B + b;
+    float Ct[d][d], cb[d];
+    ld2(Ct, C + tb * d * d);
+    ld(cb, c + tb * d);
+    float ut[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) ut[a] = 0.f;
+    if (u) ld(ut, u + tb * m);
+    if (x) {
+      float tau[d], xt[n];
+      ld(xt, x + tb * n);
+#pragma unroll
+      for (int i = 0; i < n; ++i) tau[i] = xt[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+#pragma unroll
+      for (int i = 0; i < d; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < d; ++j) s += Ct[i][j] * tau[j];
+        cb[i] = s + cb[i];
+      }
+    }
+    float Ft[n][d];
+    if (t < T - 1) {
+      ld2(Ft, F + tb * n * d);
+    } else {
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+#pragma unroll
+        for (int j = 0; j < d; ++j) Ft[i][j] = 0.f;
+    }
+    float zIt[m], lb[m], ub[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      zIt[a] = 0.f; lb[a] = 0.f; ub[a] = 0.f;
+      if constexpr (MODE == GAIN_ZERO_I) zIt[a] = zI[tb * m + a] ? 1.f : 0.f;
+      if constexpr (MODE == GAIN_BOX) {
+        lb[a] = bound_lo(bd, tb * m + a) - ut[a];
+        ub[a] = bound_hi(bd, tb * m + a) - ut[a];
+      }
+    }
+    float Kt[m][n], kt[m];
+    rs.template step<MODE>(Ct, cb, Ft, zIt, lb, ub, Kt, kt);
+    st2(K + tb * m * n, Kt);
+    st(k + tb * m, kt);
+  }
+  if (n_qp) n_qp[b] = rs.n_qp;
+}
+
+// ============================================================ forward / line search
+// lqr_forward (lqr_step_explicit.py:166-263), one problem per lane, the batch's
+// `while any(cost > old_cost)` loop evaluated per problem (each problem's alpha
+// depends only on its own cost, so this is the reference's result).
+struct NoModel {};
+
+template <int n, int m, class Model>
+struct Dyn {
+  Model md;
+  const float* F;
+  const float* f;
+  int B;
+  DEV void step(int t, int b, const float (&x)[n], const float (&uu)[m], float (&o)[n]) const {
+    if constexpr (std::is_same_v<Model, NoModel>) {
+      size_t tb = (size_t)t * B + b;
+      float Ft[n][n + m];
+      ld2(Ft, F + tb * n * (n + m));
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += Ft[i][j] * x[j];
+#pragma unroll
+        for (int j = 0; j < m; ++j) s += Ft[i][n + j] * uu[j];
+        o[i] = s;
+      }
+      if (f) {
+        float ft[n]; ld(ft, f + tb * n);
+#pragma unroll
+        for (int i = 0; i < n; ++i) o[i] += ft[i];
+      }
+    } else {
+      md.forward(x, uu, o);
+    }
+  }
+};
+
+// One rollout pass with step size alpha.  Gains come from (K,k) [T,B,m,n]/[T,B,m]
+// (GREC == 0) or from the fused kernel's per-lane gain records (GREC floats per
+// (t,b): K, k, obj_t of the current trajectory).  Returns the new cost; if
+// old_cost_out != nullptr it also returns the current trajectory's cost summed
+// in time order from the records.
+template <int n, int m, int GREC, class DynT>
+DEV float forward_pass(const DynT& dyn, int T, int B, int b, float alpha, const float* __restrict__ x_init,
+                       const float* __restrict__ C, const float* __restrict__ c, const float* __restrict__ x,
+                       const float* __restrict__ u, const float* __restrict__ K, const float* __restrict__ k,
+                       const float* __restrict__ grec, const Bounds& bd, const unsigned char* __restrict__ zI,
+                       float* __restrict__ x_out, float* __restrict__ u_out, float* __restrict__ du_sq,
+                       float* old_cost_out) {
+  constexpr int d = n + m;
+  float xn[n], dx[n];
+  ld(xn, x_init + (size_t)b * n);
+#pragma unroll
+  for (int i = 0; i < n; ++i) dx[i] = 0.f;
+  st(x_out + (size_t)b * n, xn);
+  float cost = 0.f, oldc = 0.f;
+  for (int t = 0; t < T; ++t) {
+    size_t tb = (size_t)t * B + b;
+    float Kt[m][n], kt[m], ut[m];
+    if constexpr (GREC > 0) {
+      float g[GREC];
+      ld(g, grec + tb * GREC);
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+#pragma unroll
+        for (int j = 0; j < n; ++j) Kt[a][j] = g[a * n + j];
+        kt[a] = g[m * n + a];
+      }
+      oldc += g[m * n + m];
+    } else {
+      ld2(Kt, K + tb * m * n);
+      ld(kt, k + tb * m);
+    }
+    ld(ut, u + tb * m);
+    float nu[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < n; ++j) s += Kt[a][j] * dx[j];
+      nu[a] = (s + ut[a]) + alpha * kt[a];
+      if (zI && zI[tb * m + a]) nu[a] = 0.f;
+      if (bd.mode != DILQR_BOUNDS_NONE) nu[a] = eclamp(nu[a], bound_lo(bd, tb * m + a), bound_hi(bd, tb * m + a));
+    }
+    st(u_out + tb * m, nu);
+    if (du_sq) {
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        float e = ut[a] - nu[a];
+        du_sq[((size_t)t * m + a) * B + b] = e * e;
+      }
+    }
+    float Ct[d][d], ct[d], tau[d];
+    ld2(Ct, C + tb * d * d);
+    ld(ct, c + tb * d);
+#pragma unroll
+    for (int i = 0; i < n; ++i) tau[i] = xn[i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) tau[n + a] = nu[a];
+    cost += quad_cost(Ct, ct, tau);
+    if (t < T - 1) {
+      float xnext[n], xcur[n];
+      dyn.step(t, b, xn, nu, xnext);
+      ld(xcur, x + (tb + B) * n);
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        dx[i] = xnext[i] - xcur[i];
+        xn[i] = xnext[i];
+      }
+      st(x_out + (tb + B) * n, xn);
+    }
+  }
+  if (old_cost_out) *old_cost_out = oldc;
+  return cost;
+}
+
+template <int n, int m>
+DEV float traj_cost(int T, int B, int b, const float* __restrict__ C, const float* __restrict__ c,
+                    const float* __restrict__ x, const float* __restrict__ u) {
+  constexpr int d = n + m;
+  float cost = 0.f;
+  for (int t = 0; t < T; ++t) {
+    size_t tb = (size_t)t * B + b;
+    float Ct[d][d], ct[d], tau[d], xt[n], ut[m];
+    ld2(Ct, C + tb * d * d); ld(ct, c + tb * d); ld(xt, x + tb * n); ld(ut, u + tb * m);
+#pragma unroll
+    for (int i = 0; i < n; ++i) tau[i] = xt[i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+    cost += quad_cost(Ct, ct, tau);
+  }
+  return cost;
+}
+
+template <int n, int m, class Model>
+__global__ void __launch_bounds__(kBlock) k_lqr_forward(int T, int B, const float* __restrict__ theta,
+                                                        const float* __restrict__ F, const float* __restrict__ f,
+                                                        const float* __restrict__ x_init, const float* __restrict__ C,
+                                                        const float* __restrict__ c, const float* __restrict__ x,
+                                                        const float* __restrict__ u, const float* __restrict__ K,
+                                                        const float* __restrict__ k, Bounds bd,
+                                                        const unsigned char* __restrict__ zI, float decay, int max_ls,
+                                                        float* __restrict__ x_out, float* __restrict__ u_out,
+                                                        float* __restrict__ cost_out, float* __restrict__ du_sq,
+                                                        float* __restrict__ alpha_out) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Dyn<n, m, Model> dyn;
+  if constexpr (!std::is_same_v<Model, NoModel>) dyn.md.load(theta);
+  dyn.F = F; dyn.f = f; dyn.B = B;
+  float old_cost = traj_cost<n, m>(T, B, b, C, c, x, u);        // lqr_step_explicit.py:171
+  float alpha = 1.f, cost = 0.f;
+  for (int ls = 0; ls < max_ls; ++ls) {
+    cost = forward_pass<n, m, 0>(dyn, T, B, b, alpha, x_init, C, c, x, u, K, k, nullptr, bd, zI, x_out, u_out,
+                                 ls == 0 ? du_sq : nullptr, nullptr);
+    if (!(cost > old_cost) || ls == max_ls - 1) break;
+    alpha *= decay;                                             // lqr_step_explicit.py:249
+  }
+  cost_out[b] = cost;
+  if (alpha_out) alpha_out[b] = alpha;                          // 254: the last pass's alpha
+}
+
+// ============================================================ quirk du-norm
+__global__ void __launch_bounds__(kBlock) k_quirk_norm(int TM, int B, const float* __restrict__ du_sq,
+                                                       float* __restrict__ out) {
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B) return;
+  float s = 0.f;
+  const float* p = du_sq + (size_t)r * TM;
+  for (int i = 0; i < TM; ++i) s += p[i];
+  out[r] = sqrtf(s);
+}
+
+// ============================================================ fused iLQR iteration
+// One MPC iteration body (mpc_explicit.py:249-263) for a model: linearise at the
+// current trajectory on the fly, Riccati sweep (+pnqp), the current cost, and
+// the line-search rollout.  F never touches HBM; K/k/obj_t go to a per-lane
+// record that is re-read (L2-hot) by the rollout.
+template <class Model, int MODE>
+__global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const float* __restrict__ theta,
+                                                         const float* __restrict__ x_init, const float* __restrict__ C,
+                                                         const float* __restrict__ c, const float* __restrict__ x,
+                                                         const float* __restrict__ u, Bounds bd, float decay, int max_ls,
+                                                         float* __restrict__ ws, float* __restrict__ x_out,
+                                                         float* __restrict__ u_out, float* __restrict__ cost_out,
+                                                         float* __restrict__ du_sq, float* __restrict__ alpha_out,
+                                                         const dilqr_mpc_ctrl* __restrict__ ctrl) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
+  if (ctrl && ctrl->stopped) return;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Model md; md.load(theta);
+  RiccatiState<n, m> rs;
+  rs.init();
+  for (int t = T - 1; t >= 0; --t) {
+    size_t tb = (size_t)t * B + b;
+    float Ct[d][d], ct[d], xt[n], ut[m];
+    ld2(Ct, C + tb * d * d); ld(ct, c + tb * d); ld(xt, x + tb * n); ld(ut, u + tb * m);
+    float tau[d], Ctau[d], cb[d];
+#pragma unroll
+    for (int i = 0; i < n; ++i) tau[i] = xt[i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+    float obj = quad_cost(Ct, ct, tau, Ctau);
+#pragma unroll
+    for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + ct[i];
+    float Ft[n][d];
+    if (t < T - 1) {
+      md.jacobian(xt, ut, Ft);
+    } else {
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+#pragma unroll
+        for (int j = 0; j < d; ++j) Ft[i][j] = 0.f;
+    }
+    float zIt[m], lb[m], ub[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      zIt[a] = 0.f; lb[a] = 0.f; ub[a] = 0.f;
+      if constexpr (MODE == GAIN_BOX) {
+        lb[a] = bound_lo(bd, tb * m + a) - ut[a];
+        ub[a] = bound_hi(bd, tb * m + a) - ut[a];
+      }
+    }
+    float Kt[m][n], kt[m];
+    rs.template step<MODE>(Ct, cb, Ft, zIt, lb, ub, Kt, kt);
+    float g[GREC];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+#pragma unroll
+      for (int j = 0; j < n; ++j) g[a * n + j] = Kt[a][j];
+      g[m * n + a] = kt[a];
+    }
+    g[m * n + m] = obj;
+#pragma unroll
+    for (int i = m * n + m + 1; i < GREC; ++i) g[i] = 0.f;
+    st(ws + tb * GREC, g);
+  }
+  Dyn<n, m, Model> dyn;
+  dyn.md = md; dyn.F = nullptr; dyn.f = nullptr; dyn.B = B;
+  float alpha = 1.f, cost = 0.f, old_cost = 0.f;
+  for (int ls = 0; ls < max_ls; ++ls) {
+    cost = forward_pass<n, m, GREC>(dyn, T, B, b, alpha, x_init, C, c, x, u, nullptr, nullptr, ws, bd, nullptr,
+                                    x_out, u_out, ls == 0 ? du_sq : nullptr, ls == 0 ? &old_cost : nullptr);
+    if (!(cost > old_cost) || ls == max_ls - 1) break;
+    alpha *= decay;
+  }
+  cost_out[b] = cost;
+  alpha_out[b] = alpha;
+}
+
+// ============================================================ MPC bookkeeping
+// mpc_explicit.py:264-283: full_du_norm (quirk rows), best-iterate update.
+template <int n, int m>
+__global__ void __launch_bounds__(kBlock) k_mpc_best(int T, int B, int first, float best_cost_eps,
+                                                     const float* __restrict__ x, const float* __restrict__ u,
+                                                     const float* __restrict__ cost, const float* __restrict__ du_sq,
+                                                     float* __restrict__ full_du_norm, float* __restrict__ best_x,
+                                                     float* __restrict__ best_u, float* __restrict__ best_cost,
+                                                     float* __restrict__ best_du, dilqr_mpc_ctrl* __restrict__ ctrl) {
+  if (ctrl->stopped) return;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int TM = T * m;
+  float s = 0.f;
+  const float* p = du_sq + (size_t)b * TM;
+  for (int i = 0; i < TM; ++i) s += p[i];
+  float fdn = sqrtf(s);
+  full_du_norm[b] = fdn;
+  atomicMax(&ctrl->max_du_bits, __float_as_uint(fdn));
+  float cb = cost[b];
+  bool take = first != 0;
+  if (!take && cb <= best_cost[b] + best_cost_eps) {
+    take = true;
+    atomicOr(&ctrl->any_improved, 1);
+  }
+  if (take) {
+    best_cost[b] = cb;
+    best_du[b] = fdn;
+    for (int t = 0; t < T; ++t) {
+      size_t tb = (size_t)t * B + b;
+      float xt[n], ut[m];
+      ld(xt, x + tb * n); ld(ut, u + tb * m);
+      st(best_x + tb * n, xt); st(best_u + tb * m, ut);
+    }
+  }
+}
+
+// mpc_explicit.py:264, 279, 297-299
+__global__ void k_mpc_control(int first, float eps, int not_improved_lim, dilqr_mpc_ctrl* ctrl) {
+  if (ctrl->stopped) return;
+  ctrl->iter += 1;
+  ctrl->n_not_improved += 1;
+  if (!first && ctrl->any_improved) ctrl->n_not_improved = 0;
+  float mx = __uint_as_float(ctrl->max_du_bits);
+  if (mx < eps || ctrl->n_not_improved > not_improved_lim) ctrl->stopped = 1;
+  ctrl->any_improved = 0;
+  ctrl->max_du_bits = 0u;
+}
+
+// ============================================================ classic adjoint
+// lqr_step.py:312-407 for one problem per lane:
+//   phase 1: Riccati sweep of the adjoint problem (c_back = -r, u_zero_I = active set)
+//   phase 2: its LinDx rollout from 0 with the default line search (decay 0.2, 10
+//            passes; old cost 0), d tau stored as dc = -d tau
+//   phase 3: costates lam, dlam backwards; dC, dF, df, dx_init.
+template <int n, int m, int MODE>
+__global__ void __launch_bounds__(kBlock) k_lqr_adjoint(int T, int B, const float* __restrict__ C,
+                                                        const float* __restrict__ c, const float* __restrict__ F,
+                                                        const float* __restrict__ x, const float* __restrict__ u,
+                                                        const float* __restrict__ dl_dx, const float* __restrict__ dl_du,
+                                                        Bounds bd, float* __restrict__ ws, float* __restrict__ dx_init,
+                                                        float* __restrict__ dC, float* __restrict__ dc,
+                                                        float* __restrict__ dF, float* __restrict__ df) {
+  constexpr int d = n + m;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  // active set (lqr_step.py:321-325)
+  auto active = [&](size_t tb, int a) -> bool {
+    if (bd.mode == DILQR_BOUNDS_NONE) return false;
+    float ua = u[tb * m + a];
+    return fabsf(ua - bound_lo(bd, tb * m + a)) <= 1e-8f || fabsf(ua - bound_hi(bd, tb * m + a)) <= 1e-8f;
+  };
+  // ---- phase 1
+  RiccatiState<n, m> rs;
+  rs.init();
+  for (int t = T - 1; t >= 0; --t) {
+    size_t tb = (size_t)t * B + b;
+    float Ct[d][d], cb[d], rx[n], ru[m];
+    ld2(Ct, C + tb * d * d);
+    ld(rx, dl_dx + tb * n); ld(ru, dl_du + tb * m);
+#pragma unroll
+    for (int i = 0; i < n; ++i) cb[i] = -rx[i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) cb[n + a] = -ru[a];
+    float Ft[n][d];
+    if (t < T - 1) {
+      ld2(Ft, F + tb * n * d);
+    } else {
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+#pragma unroll
+        for (int j = 0; j < d; ++j) Ft[i][j] = 0.f;
+    }
+    float zIt[m], lb[m], ub[m];
+    bool any = false;
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      zIt[a] = active(tb, a) ? 1.f : 0.f;
+      any |= zIt[a] != 0.f;
+      lb[a] = ub[a] = 0.f;
+    }
+    float Kt[m][n], kt[m];
+    if (bd.mode != DILQR_BOUNDS_NONE) rs.template step<GAIN_ZERO_I>(Ct, cb, Ft, zIt, lb, ub, Kt, kt);
+    else rs.template step<MODE>(Ct, cb, Ft, zIt, lb, ub, Kt, kt);
+    (void)any;
+    st2(ws + tb * (m * n + m), Kt);
+    st(ws + tb * (m * n + m) + m * n, kt);
+  }
+  // ---- phase 2: rollout of the adjoint LQR from zero with line search
+  float alpha = 1.f;
+  for (int ls = 0; ls < 10; ++ls) {
+    float xn[n], cost = 0.f;
+#pragma unroll
+    for (int i = 0; i < n; ++i) xn[i] = 0.f;
+    for (int t = 0; t < T; ++t) {
+      size_t tb = (size_t)t * B + b;
+      float Kt[m][n], kt[m], nu[m];
+      ld2(Kt, ws + tb * (m * n + m));
+      ld(kt, ws + tb * (m * n + m) + m * n);
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += Kt[a][j] * xn[j];       // dx = new_x - 0
+        nu[a] = (s + 0.f) + alpha * kt[a];
+        if (active(tb, a)) nu[a] = 0.f;
+      }
+      float tau[d], Ct[d][d], rr[d];
+#pragma unroll
+      for (int i = 0; i < n; ++i) tau[i] = xn[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) tau[n + a] = nu[a];
+      float ndt[d];
+#pragma unroll
+      for (int i = 0; i < d; ++i) ndt[i] = -tau[i];
+      st(dc + tb * d, ndt);
+      ld2(Ct, C + tb * d * d);
+      {
+        float rx[n], ru[m];
+        ld(rx, dl_dx + tb * n); ld(ru, dl_du + tb * m);
+#pragma unroll
+        for (int i = 0; i < n; ++i) rr[i] = -rx[i];
+#pragma unroll
+        for (int a = 0; a < m; ++a) rr[n + a] = -ru[a];
+      }
+      cost += quad_cost(Ct, rr, tau);
+      if (t < T - 1) {
+        float Ft[n][d];
+        ld2(Ft, F + tb * n * d);
+        float xnext[n];
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < d; ++j) s += Ft[i][j] * tau[j];
+          xnext[i] = s;
+        }
+#pragma unroll
+        for (int i = 0; i < n; ++i) xn[i] = xnext[i];
+      }
+    }
+    if (!(cost > 0.f) || ls == 9) break;
+    alpha *= 0.2f;
+  }
+  // ---- phase 3: costates and gradients (lqr_step.py:352-405)
+  float lam[n], dlam[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) lam[i] = dlam[i] = 0.f;
+  for (int t = T - 1; t >= 0; --t) {
+    size_t tb = (size_t)t * B + b;
+    float Ct[d][d], ctt[d], xt[n], ut[m], tau[d], dtau[d], rx[n];
+    ld2(Ct, C + tb * d * d); ld(ctt, c + tb * d); ld(xt, x + tb * n); ld(ut, u + tb * m);
+    ld(dtau, dc + tb * d);
+    ld(rx, dl_dx + tb * n);
+#pragma unroll
+    for (int i = 0; i < d; ++i) dtau[i] = -dtau[i];
+#pragma unroll
+    for (int i = 0; i < n; ++i) tau[i] = xt[i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+    // dC_t = -0.5 (dtau tau^T + tau dtau^T)
+    float dCt[d][d];
+#pragma unroll
+    for (int i = 0; i < d; ++i)
+#pragma unroll
+      for (int j = 0; j < d; ++j) dCt[i][j] = -0.5f * (dtau[i] * tau[j] + tau[i] * dtau[j]);
+    st2(dC + tb * d * d, dCt);
+    if (t < T - 1) {
+      // dF_t = -(dlam_{t+1} tau_t^T + lam_{t+1} dtau_t^T); df_t = -dlam_{t+1}
+      float dFt[n][d], dft[n];
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+#pragma unroll
+        for (int j = 0; j < d; ++j) dFt[i][j] = -(dlam[i] * tau[j] + lam[i] * dtau[j]);
+        dft[i] = -dlam[i];
+      }
+      st2(dF + tb * n * d, dFt);
+      if (df) st(df + tb * n, dft);
+    }
+    // lam_t = Cxx x + Cxu u + c_x + F_x^T lam_{t+1}; dlam likewise with dtau and -r_x
+    float nl[n], ndl[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < n; ++j) { s1 += Ct[i][j] * xt[j]; s2 += Ct[i][j] * dtau[j]; }
+      float s3 = 0.f, s4 = 0.f;
+#pragma unroll
+      for (int a = 0; a < m; ++a) { s3 += Ct[i][n + a] * ut[a]; s4 += Ct[i][n + a] * dtau[n + a]; }
+      nl[i] = (s1 + s3) + ctt[i];
+      ndl[i] = (s2 + s4) - rx[i];
+    }
+    if (t < T - 1) {
+      float Ft[n][d];
+      ld2(Ft, F + tb * n * d);
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int l = 0; l < n; ++l) { s1 += Ft[l][i] * lam[l]; s2 += Ft[l][i] * dlam[l]; }
+        nl[i] += s1;
+        ndl[i] += s2;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < n; ++i) { lam[i] = nl[i]; dlam[i] = ndl[i]; }
+  }
+  float dxi[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) dxi[i] = -dlam[i];
+  st(dx_init + (size_t)b * n, dxi);
+}
+
+}  // namespace dilqr
+
+// ====================================================================== C-ABI
+using namespace dilqr;
+
+namespace {
+
+inline int herr(hipError_t e) { return e == hipSuccess ? 0 : -(int)e; }
+inline int launched() { return herr(hipGetLastError()); }
+inline bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline Bounds mkb(const dilqr_bounds& b) { return Bounds{b.mode, b.lo, b.hi, b.lo_t, b.hi_t}; }
+inline bool bad_bounds(const dilqr_bounds& b) {
+  if (b.mode == DILQR_BOUNDS_TENSOR) return !b.lo_t || !b.hi_t;
+  return b.mode != DILQR_BOUNDS_NONE && b.mode != DILQR_BOUNDS_SCALAR;
+}
+
+// (n, m) shapes compiled for the generic (LinDx / Riccati / adjoint) kernels.
+// Model kernels use their own fixed shapes.
+#define DILQR_FOR_EACH_SHAPE(X) X(3, 1) X(5, 1) X(4, 3) X(4, 1) X(2, 1) X(4, 2) X(6, 2)
+
+}  // namespace
+
+extern "C" {
+
+int dilqr_version(void) { return 1; }
+
+int dilqr_model_num_params(int model) {
+  switch (model) {
+    case DILQR_MODEL_PENDULUM: return Pendulum::P;
+    case DILQR_MODEL_CARTPOLE: return Cartpole::P;
+    default: return -1;
+  }
+}
+
+#define MODEL_SWITCH(model, CALL)                       \
+  switch (model) {                                      \
+    case DILQR_MODEL_PENDULUM: { using MD = Pendulum; CALL; break; } \
+    case DILQR_MODEL_CARTPOLE: { using MD = Cartpole; CALL; break; } \
+    default: return DILQR_E_SHAPE;                      \
+  }
+
+int dilqr_dynamics_f32(int model, int N, const float* theta, const float* x, const float* u, float* out,
+                       void* stream) {
+  if (N < 0 || !theta || !x || !u || !out) return DILQR_E_ARG;
+  if (N == 0) return 0;
+  MODEL_SWITCH(model, (k_dynamics<MD><<<grid_for(N), kBlock, 0, S(stream)>>>(N, theta, x, u, out)));
+  return launched();
+}
+
+int dilqr_linear_dyn_f32(int model, int N, const float* theta, const float* x, const float* u, float* D,
+                         void* stream) {
+  if (N < 0 || !theta || !x || !u || !D) return DILQR_E_ARG;
+  if (N == 0) return 0;
+  MODEL_SWITCH(model, (k_linear_dyn<MD><<<grid_for(N), kBlock, 0, S(stream)>>>(N, theta, x, u, D)));
+  return launched();
+}
+
+int dilqr_rollout_f32(int model, int n, int m, int T, int B, const float* theta, const float* F, const float* f,
+                      const float* x_init, const float* u, float* x_out, void* stream) {
+  if (T < 1 || B < 0 || !x_init || !u || !x_out) return DILQR_E_ARG;
+  if (!al16(F) || !al16(f) || !al16(x_init) || !al16(u) || !al16(x_out)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  if (model == DILQR_MODEL_LINDX) {
+    if (!F && T > 1) return DILQR_E_ARG;
+#define X(N_, M_) \
+    if (n == N_ && m == M_) { k_rollout_lin<N_, M_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, F, f, x_init, u, x_out); return launched(); }
+    DILQR_FOR_EACH_SHAPE(X)
+#undef X
+    return DILQR_E_SHAPE;
+  }
+  if (!theta) return DILQR_E_ARG;
+  MODEL_SWITCH(model, (k_rollout<MD><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, u, x_out)));
+  return launched();
+}
+
+int dilqr_linearize_f32(int model, int T, int B, const float* theta, const float* x, const float* u, float* F,
+                        float* f, void* stream) {
+  if (T < 1 || B < 0 || !theta || !x || !u || !F || !f) return DILQR_E_ARG;
+  long long N = (long long)(T - 1) * B;
+  if (N == 0) return 0;
+  MODEL_SWITCH(model, (k_linearize<MD><<<grid_for(N), kBlock, 0, S(stream)>>>(T, B, theta, x, u, F, f)));
+  return launched();
+}
+
+int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const float* c, const float* x,
+                           const float* u, const float* F, dilqr_bounds bounds, const unsigned char* u_zero_I,
+                           int m_solver, float* K, float* k, int* n_qp_iter, void* stream) {
+  if (T < 1 || B < 0 || !C || !c || !K || !k || (T > 1 && !F)) return DILQR_E_ARG;
+  if (x && !u) return DILQR_E_ARG;   // u alone: c is already c_back, u only shifts the bounds
+  if (!al16(C) || !al16(c) || !al16(x) || !al16(u) || !al16(F) || !al16(K) || !al16(k)) return DILQR_E_ARG;
+  if (bad_bounds(bounds)) return DILQR_E_ARG;
+  if (bounds.mode != DILQR_BOUNDS_NONE && (u_zero_I || !u)) return DILQR_E_MODE;
+  if (B == 0) return 0;
+  Bounds bd = mkb(bounds);
+  int mode = bounds.mode != DILQR_BOUNDS_NONE ? GAIN_BOX
+             : u_zero_I ? GAIN_ZERO_I
+             : (m_solver == DILQR_SOLVE_CHOL && m > 1) ? GAIN_CHOL : GAIN_UNC;
+#define LAUNCH(N_, M_, MODE_) \
+  k_lqr_backward<N_, M_, MODE_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, C, c, x, u, F, bd, u_zero_I, K, k, n_qp_iter)
+#define X(N_, M_)                                              \
+  if (n == N_ && m == M_) {                                    \
+    switch (mode) {                                            \
+      case GAIN_UNC: LAUNCH(N_, M_, GAIN_UNC); break;          \
+      case GAIN_CHOL: LAUNCH(N_, M_, GAIN_CHOL); break;        \
+      case GAIN_ZERO_I: LAUNCH(N_, M_, GAIN_ZERO_I); break;    \
+      default: LAUNCH(N_, M_, GAIN_BOX); break;                \
+    }                                                          \
+    return launched();                                         \
+  }
+  DILQR_FOR_EACH_SHAPE(X)
+#undef X
+#undef LAUNCH
+  return DILQR_E_SHAPE;
+}
+
+int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* theta, const float* F, const float* f,
+                          const float* x_init, const float* C, const float* c, const float* x, const float* u,
+                          const float* K, const float* k, dilqr_bounds bounds, const unsigned char* u_zero_I,
+                          float linesearch_decay, int max_linesearch_iter, float* x_out, float* u_out, float* cost,
+                          float* du_sq, float* alpha, void* stream) {
+  if (T < 1 || B < 0 || max_linesearch_iter < 1) return DILQR_E_ARG;
+  if (!x_init || !C || !c || !x || !u || !K || !k || !x_out || !u_out || !cost) return DILQR_E_ARG;
+  const void* ps[] = {F, f, x_init, C, c, x, u, K, k, x_out, u_out};
+  for (const void* p : ps) if (!al16(p)) return DILQR_E_ARG;
+  if (bad_bounds(bounds)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  Bounds bd = mkb(bounds);
+  if (model == DILQR_MODEL_LINDX) {
+    if (!F && T > 1) return DILQR_E_ARG;
+#define X(N_, M_)                                                                                             \
+    if (n == N_ && m == M_) {                                                                                  \
+      k_lqr_forward<N_, M_, NoModel><<<grid_for(B), kBlock, 0, S(stream)>>>(                                   \
+          T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter,     \
+          x_out, u_out, cost, du_sq, alpha);                                                                   \
+      return launched();                                                                                       \
+    }
+    DILQR_FOR_EACH_SHAPE(X)
+#undef X
+    return DILQR_E_SHAPE;
+  }
+  if (!theta) return DILQR_E_ARG;
+  MODEL_SWITCH(model, ({
+    if (n != MD::N || m != MD::M) return DILQR_E_SHAPE;
+    k_lqr_forward<MD::N, MD::M, MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
+        T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter, x_out,
+        u_out, cost, du_sq, alpha);
+  }));
+  return launched();
+}
+
+int dilqr_quirk_norm_f32(int T, int m, int B, const float* du_sq, float* out, void* stream) {
+  if (T < 1 || m < 1 || B < 0 || !du_sq || !out) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  k_quirk_norm<<<grid_for(B), kBlock, 0, S(stream)>>>(T * m, B, du_sq, out);
+  return launched();
+}
+
+int dilqr_ilqr_iterate_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
+                           const float* c, const float* x, const float* u, dilqr_bounds bounds,
+                           float linesearch_decay, int max_linesearch_iter, float* ws_gains, float* x_out,
+                           float* u_out, float* cost, float* du_sq, float* alpha, dilqr_mpc_ctrl* ctrl,
+                           void* stream) {
+  if (T < 1 || B < 0 || max_linesearch_iter < 1) return DILQR_E_ARG;
+  if (!theta || !x_init || !C || !c || !x || !u || !ws_gains || !x_out || !u_out || !cost || !du_sq || !alpha)
+    return DILQR_E_ARG;
+  const void* ps[] = {x_init, C, c, x, u, ws_gains, x_out, u_out};
+  for (const void* p : ps) if (!al16(p)) return DILQR_E_ARG;
+  if (bad_bounds(bounds)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  Bounds bd = mkb(bounds);
+  bool box = bounds.mode != DILQR_BOUNDS_NONE;
+  MODEL_SWITCH(model, ({
+    if (box)
+      k_ilqr_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(
+          T, B, theta, x_init, C, c, x, u, bd, linesearch_decay, max_linesearch_iter, ws_gains, x_out, u_out, cost,
+          du_sq, alpha, ctrl);
+    else
+      k_ilqr_iterate<MD, GAIN_UNC><<<grid_for(B), kBlock, 0, S(stream)>>>(
+          T, B, theta, x_init, C, c, x, u, bd, linesearch_decay, max_linesearch_iter, ws_gains, x_out, u_out, cost,
+          du_sq, alpha, ctrl);
+  }));
+  return launched();
+}
+
+int dilqr_mpc_update_best_f32(int n, int m, int T, int B, int first, float best_cost_eps, float eps,
+                              int not_improved_lim, const float* x, const float* u, const float* cost,
+                              const float* du_sq, float* full_du_norm, float* best_x, float* best_u,
+                              float* best_cost, float* best_du, dilqr_mpc_ctrl* ctrl, void* stream) {
+  if (T < 1 || B < 0 || !x || !u || !cost || !du_sq || !full_du_norm || !best_x || !best_u || !best_cost ||
+      !best_du || !ctrl)
+    return DILQR_E_ARG;
+  if (!al16(x) || !al16(u) || !al16(best_x) || !al16(best_u)) return DILQR_E_ARG;
+  if (B > 0) {
+    bool ok = false;
+#define X(N_, M_)                                                                                        \
+    if (!ok && n == N_ && m == M_) {                                                                      \
+      k_mpc_best<N_, M_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, first, best_cost_eps, x, u, cost, du_sq, \
+                                                                full_du_norm, best_x, best_u, best_cost,  \
+                                                                best_du, ctrl);                           \
+      ok = true;                                                                                          \
+    }
+    DILQR_FOR_EACH_SHAPE(X)
+#undef X
+    if (!ok) return DILQR_E_SHAPE;
+    int e = launched();
+    if (e) return e;
+  }
+  k_mpc_control<<<1, 1, 0, S(stream)>>>(first, eps, not_improved_lim, ctrl);
+  return launched();
+}
+
+int dilqr_lqr_adjoint_f32(int n, int m, int T, int B, const float* C, const float* c, const float* F,
+                          const float* x, const float* u, const float* dl_dx, const float* dl_du, dilqr_bounds bounds,
+                          int m_solver, float* ws, float* dx_init, float* dC, float* dc, float* dF, float* df,
+                          void* stream) {
+  if (T < 1 || B < 0 || !C || !c || !x || !u || !dl_dx || !dl_du || !ws || !dx_init || !dC || !dc) return DILQR_E_ARG;
+  if (T > 1 && (!F || !dF)) return DILQR_E_ARG;
+  const void* ps[] = {C, c, F, x, u, dl_dx, dl_du, ws, dx_init, dC, dc, dF, df};
+  for (const void* p : ps) if (!al16(p)) return DILQR_E_ARG;
+  if (bad_bounds(bounds)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  Bounds bd = mkb(bounds);
+  bool chol = m_solver == DILQR_SOLVE_CHOL && m > 1;
+#define X(N_, M_)                                                                                           \
+  if (n == N_ && m == M_) {                                                                                  \
+    if (chol)                                                                                                \
+      k_lqr_adjoint<N_, M_, GAIN_CHOL><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, C, c, F, x, u, dl_dx,    \
+                                                                             dl_du, bd, ws, dx_init, dC, dc, \
+                                                                             dF, df);                        \
+    else                                                                                                     \
+      k_lqr_adjoint<N_, M_, GAIN_UNC><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, C, c, F, x, u, dl_dx,     \
+                                                                            dl_du, bd, ws, dx_init, dC, dc,  \
+                                                                            dF, df);                         \
+    return launched();                                                                                       \
+  }
+  DILQR_FOR_EACH_SHAPE(X)
+#undef X
+  return DILQR_E_SHAPE;
+}
+
+}  // extern "C"

@@ -1,0 +1,42 @@
+"""Shared model plumbing: every model's forward / get_linear_dyn runs on the GPU
+through libdilqr.so; the module holds the reference's constants."""
+import torch
+from torch import nn
+
+from .. import _native as N
+
+
+class HipDynamics(nn.Module):
+    model_id = None
+    n_state = n_ctrl = None
+
+    def _theta(self, like):
+        p = self.params
+        if not isinstance(p, torch.Tensor):
+            p = torch.tensor(p)
+        return p.detach().to(device=like.device, dtype=torch.float32).contiguous()
+
+    def forward(self, x, u):
+        squeeze = x.ndimension() == 1
+        if squeeze:
+            x, u = x.unsqueeze(0), u.unsqueeze(0)
+        x = x.detach().contiguous()
+        u = u.detach().contiguous()
+        out = torch.empty_like(x)
+        N.call("dilqr_dynamics_f32", self.model_id, x.shape[0], N.ptr(self._theta(x)), N.ptr(x), N.ptr(u),
+               N.ptr(out), N.stream(x.device))
+        return out.squeeze(0) if squeeze else out
+
+    def get_linear_dyn(self, x, u):
+        x = x.detach().contiguous()
+        u = u.detach().contiguous()
+        D = torch.empty(x.shape[0], self.n_state, self.n_state + self.n_ctrl, device=x.device)
+        N.call("dilqr_linear_dyn_f32", self.model_id, x.shape[0], N.ptr(self._theta(x)), N.ptr(x), N.ptr(u),
+               N.ptr(D), N.stream(x.device))
+        return D
+
+    def get_true_obj(self):
+        q = torch.cat((self.goal_weights, self.ctrl_penalty * torch.ones(self.n_ctrl)))
+        px = -torch.sqrt(self.goal_weights) * self.goal_state
+        p = torch.cat((px, torch.zeros(self.n_ctrl)))
+        return q, p

@@ -1,0 +1,64 @@
+"""Classic differentiable LQR step of mpc.pytorch (lqr_step.py:23-409) on the HIP path.
+
+`LQRStep(...)` returns `apply(x_init, C, c, F, f=None)`; forward is the same
+Riccati sweep + line-search rollout as the DiLQR step, backward is the classic
+adjoint (lqr_step.py:312-407) returning (dx_init, dC, dc, dF, df), computed by
+one fused kernel (dilqr_lqr_adjoint_f32).
+"""
+import torch
+from torch.autograd import Function
+
+from . import _native as N
+from . import ops
+from .definitions import QuadCost
+
+
+def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta_u=None,
+            linesearch_decay=0.2, max_linesearch_iter=10, true_cost=None, true_dynamics=None,
+            delta_space=True, current_x=None, current_u=None, verbose=0, back_eps=1e-3,
+            no_op_forward=False):
+    if delta_u is not None:
+        raise NotImplementedError("dilqr: delta_u is not on the HIP path")
+    if not delta_space:
+        raise NotImplementedError("dilqr: delta_space=False is unimplemented in the reference too")
+    if u_zero_I is not None:
+        raise NotImplementedError("dilqr: u_zero_I is only used inside the adjoint engine")
+    lo = u_lower if (u_lower is None or isinstance(u_lower, (int, float))) else u_lower.detach()
+    hi = u_upper if (u_upper is None or isinstance(u_upper, (int, float))) else u_upper.detach()
+
+    class LQRStepFn(Function):
+        @staticmethod
+        def forward(ctx, x_init, C, c, F, f=None):
+            x, u = current_x.detach(), current_u.detach()
+            if no_op_forward:                                   # lqr_step.py:277-282
+                ctx.save_for_backward(x_init, C, c, F, f, x, u)
+                return x.clone(), u.clone()
+            if not isinstance(true_cost, QuadCost):
+                raise NotImplementedError("dilqr: true_cost must be a QuadCost on the HIP path")
+            m_id = ops.model_id_of(true_dynamics)
+            K, k, nqp = ops.lqr_backward(C, c, F, n_state, n_ctrl, x=x, u=u, u_lower=lo, u_upper=hi,
+                                         want_nqp=lo is not None)
+            if m_id == N.MODEL_LINDX:
+                th, Fd, fd = None, true_dynamics.F, true_dynamics.f
+                if fd is not None and fd.nelement() == 0:
+                    fd = None
+            else:
+                th, Fd, fd = ops.theta_of(true_dynamics, x_init), None, None
+            Ct, ct = true_cost
+            nx, nu, costs, du_sq, alphas = ops.lqr_forward(
+                m_id, th, x_init, Ct, ct, x, u, K, k, F=Fd, f=fd, u_lower=lo, u_upper=hi,
+                linesearch_decay=linesearch_decay, max_linesearch_iter=max_linesearch_iter)
+            full_du_norm = ops.quirk_norm(du_sq)
+            n_qp = int(nqp.max().item()) if nqp is not None else 0
+            ctx.save_for_backward(x_init, C, c, F, f, nx, nu)
+            return nx, nu, torch.tensor([float(n_qp)]), costs, full_du_norm, alphas.mean()
+
+        @staticmethod
+        def backward(ctx, dl_dx, dl_du, *unused):
+            x_init, C, c, F, f, nx, nu = ctx.saved_tensors
+            has_f = f is not None and f.nelement() > 0
+            dx0, dC, dc, dF, df = ops.lqr_adjoint(C, c, F, nx, nu, dl_dx.contiguous(), dl_du.contiguous(),
+                                                  u_lower=lo, u_upper=hi, m_solver=N.SOLVE_INV, want_df=has_f)
+            return dx0, dC, dc, dF, (df if has_f else None)
+
+    return LQRStepFn.apply

@@ -1,0 +1,82 @@
+"""LQRStep of DiLQR (lqr_step_explicit.py:24-718) on the HIP path.
+
+`LQRStep(...)` returns a callable with the reference's signature
+`apply(x_init, C, c, F, f=None, theta=None)`:
+
+  * regular forward  -> (new_x, new_u, Tensor([n_total_qp_iter]), costs,
+                         full_du_norm, mean_alphas)      (lqr_step_explicit.py:625-650)
+  * no_op_forward    -> (current_x, current_u) with the Riccati gains of the
+                         current trajectory saved for the implicit backward
+                         (lqr_step_explicit.py:604-623)
+
+The backward of the no-op step is the DiLQR implicit differentiation
+(lqr_step_explicit.py:653-712) and returns (None, dC, dc, None, None,
+dtheta [B,p], None); autograd sums dtheta over the batch like the reference.
+"""
+import torch
+from torch.autograd import Function
+
+from . import _native as N
+from . import ops
+from .definitions import LinDx, QuadCost
+
+
+def _bounds_arg(v):
+    if v is None or isinstance(v, (int, float)):
+        return v
+    return v.detach()
+
+
+def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta_u=None,
+            linesearch_decay=0.2, max_linesearch_iter=10, true_cost=None, true_dynamics=None,
+            delta_space=True, current_x=None, current_u=None, verbose=0, back_eps=1e-3,
+            no_op_forward=False, theta=None):
+    if delta_u is not None:
+        raise NotImplementedError("dilqr: delta_u is not on the HIP path")
+    if not delta_space:
+        raise NotImplementedError("dilqr: delta_space=False is unimplemented in the reference too (639)")
+    lo, hi = _bounds_arg(u_lower), _bounds_arg(u_upper)
+
+    class LQRStepFn(Function):
+        @staticmethod
+        def forward(ctx, x_init, C, c, F, f=None, theta=None, if_converge=False):
+            assert current_x is not None and current_u is not None
+            x, u = current_x.detach(), current_u.detach()
+            m_id = ops.model_id_of(true_dynamics)
+            if no_op_forward:
+                K, _, _ = ops.lqr_backward(C, c, F, n_state, n_ctrl, x=x, u=u, u_lower=lo, u_upper=hi,
+                                           u_zero_I=u_zero_I)
+                ctx.save_for_backward(x_init, C, c, F, f, x, u, theta, K)
+                ctx.model = true_dynamics
+                return x.clone(), u.clone()
+            if not isinstance(true_cost, QuadCost):
+                raise NotImplementedError("dilqr: true_cost must be a QuadCost on the HIP path")
+            K, k, nqp = ops.lqr_backward(C, c, F, n_state, n_ctrl, x=x, u=u, u_lower=lo, u_upper=hi,
+                                         u_zero_I=u_zero_I, want_nqp=lo is not None)
+            if m_id == N.MODEL_LINDX:
+                th, Fd, fd = None, true_dynamics.F, true_dynamics.f
+                if fd is not None and fd.nelement() == 0:
+                    fd = None
+            else:
+                th, Fd, fd = ops.theta_of(true_dynamics, x_init), None, None
+            Ct, ct = true_cost
+            nx, nu, costs, du_sq, alphas = ops.lqr_forward(
+                m_id, th, x_init, Ct, ct, x, u, K, k, F=Fd, f=fd, u_lower=lo, u_upper=hi, u_zero_I=u_zero_I,
+                linesearch_decay=linesearch_decay, max_linesearch_iter=max_linesearch_iter)
+            full_du_norm = ops.quirk_norm(du_sq)
+            n_qp = int(nqp.max().item()) if nqp is not None else 0
+            ctx.save_for_backward(x_init, C, c, F, f, nx, nu)
+            return nx, nu, torch.tensor([float(n_qp)]), costs, full_du_norm, alphas.mean()
+
+        @staticmethod
+        def backward(ctx, dl_dx, dl_du, *unused):
+            if len(ctx.saved_tensors) != 9:
+                # the reference's backward unpacks 9 saved tensors and fails the
+                # same way after a regular (non no-op) forward (656)
+                raise RuntimeError("LQRStep backward needs a no_op_forward step (lqr_step_explicit.py:656)")
+            from .implicit import implicit_backward
+            x_init, C, c, F, f, x, u, th, K = ctx.saved_tensors
+            dC, dc, dtheta = implicit_backward(ctx.model, dl_dx, dl_du, C, c, F, f, x, u, K, lo, hi, th)
+            return None, dC, dc, None, None, dtheta, None
+
+    return LQRStepFn.apply

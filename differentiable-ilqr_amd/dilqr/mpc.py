@@ -1,0 +1,90 @@
+"""Classic mpc.pytorch MPC (mpc.py:57-601) on the HIP path.
+
+Takes model dynamics or a LinDx.  The forward loop runs on device; gradients
+flow through a no-op classic LQR step (lqr_step.py:277-282) whose backward is
+the classic adjoint kernel, exactly like mpc.py:302-335.  With model dynamics
+the reference would also differentiate the autograd linearisation
+(mpc.py:538-551); on the HIP path F, f are kernel outputs, so gradients reach
+(x_init, C, c) and, for LinDx, (F, f).
+"""
+import warnings
+
+import torch
+from torch.nn import Module
+
+from . import _native as N
+from . import ops
+from .definitions import LinDx, QuadCost
+from .lqr_step import LQRStep
+from .mpc_explicit import GradMethods, expand_cost
+
+
+class MPC(Module):
+    def __init__(self, n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, u_init=None,
+                 lqr_iter=10, grad_method=GradMethods.ANALYTIC, delta_u=None, verbose=0, eps=1e-7,
+                 back_eps=1e-7, n_batch=None, linesearch_decay=0.2, max_linesearch_iter=10,
+                 exit_unconverged=True, detach_unconverged=True, backprop=True, slew_rate_penalty=None,
+                 prev_ctrl=None, not_improved_lim=5, best_cost_eps=1e-4):
+        super().__init__()
+        assert (u_lower is None) == (u_upper is None)
+        assert max_linesearch_iter > 0
+        for name, val in (("u_zero_I", u_zero_I), ("delta_u", delta_u), ("slew_rate_penalty", slew_rate_penalty)):
+            if val is not None:
+                raise NotImplementedError(f"dilqr: MPC({name}=...) is not on the HIP path")
+        self.n_state, self.n_ctrl, self.T = n_state, n_ctrl, T
+        self.u_lower = u_lower if (u_lower is None or isinstance(u_lower, float)) else u_lower.detach()
+        self.u_upper = u_upper if (u_upper is None or isinstance(u_upper, float)) else u_upper.detach()
+        self.u_init = None if u_init is None else u_init.detach()
+        self.lqr_iter, self.grad_method, self.verbose = lqr_iter, grad_method, verbose
+        self.eps, self.back_eps, self.n_batch = eps, back_eps, n_batch
+        self.linesearch_decay, self.max_linesearch_iter = linesearch_decay, max_linesearch_iter
+        self.exit_unconverged, self.detach_unconverged, self.backprop = exit_unconverged, detach_unconverged, backprop
+        self.not_improved_lim, self.best_cost_eps = not_improved_lim, best_cost_eps
+
+    def forward(self, x_init, cost, dx):
+        if not isinstance(cost, QuadCost):
+            raise NotImplementedError("dilqr: non-quadratic costs are not on the HIP path")
+        if not x_init.is_cuda:
+            raise RuntimeError("dilqr: x_init must be on the GPU (no CPU path)")
+        n_batch = self.n_batch if self.n_batch is not None else (
+            cost.C.size(1) if cost.C.ndimension() == 4 else None)
+        if n_batch is None:
+            raise ValueError("MPC Error: Could not infer batch size, pass in as n_batch")
+        T, n, m = self.T, self.n_state, self.n_ctrl
+        C, c = expand_cost(cost.C, cost.c, T, n_batch, n + m)
+        model_id = ops.model_id_of(dx)
+        lin = model_id == N.MODEL_LINDX
+        theta = None if lin else ops.theta_of(dx, x_init)
+        Fd = fd = None
+        if lin:
+            Fd = dx.F.detach().contiguous()
+            fd = None if (dx.f is None or dx.f.nelement() == 0) else dx.f.detach().contiguous()
+        with torch.no_grad():
+            ws = ops.mpc_solve_unfused(model_id, theta, x_init.detach(), C.detach().contiguous(),
+                                       c.detach().contiguous(), T, F=Fd, f=fd, u_init=self.u_init,
+                                       u_lower=self.u_lower, u_upper=self.u_upper, lqr_iter=self.lqr_iter,
+                                       eps=self.eps, linesearch_decay=self.linesearch_decay,
+                                       max_linesearch_iter=self.max_linesearch_iter,
+                                       not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps)
+        x, u, costs, full_du_norm = ws.best_x, ws.best_u, ws.best_cost, ws.best_du
+        if torch.is_grad_enabled() and self.backprop:
+            if lin:
+                F, f = dx.F, (dx.f if dx.f is not None else torch.empty(0, device=x.device))
+            else:
+                F, f = ops.linearize(model_id, theta, x, u)
+            step = LQRStep(n, m, T, u_lower=self.u_lower, u_upper=self.u_upper, true_cost=QuadCost(C, c),
+                           true_dynamics=dx, current_x=x, current_u=u, back_eps=self.back_eps,
+                           no_op_forward=True)
+            x, u = step(x_init, C, c, F, f)
+        if self.detach_unconverged and float(full_du_norm.max()) > self.eps:    # mpc.py:321-334
+            if self.exit_unconverged:
+                raise AssertionError("LQR did not converge (exit_unconverged=True)")
+            if self.verbose >= 0:
+                warnings.warn("LQR Warning: All examples did not converge to a fixed point. "
+                              "Detaching and *not* backpropping through the bad examples.")
+            I = (full_du_norm < self.eps)
+            Ix = I.view(1, -1, 1).expand_as(x).to(x.dtype)
+            Iu = I.view(1, -1, 1).expand_as(u).to(u.dtype)
+            x = x * Ix + x.clone().detach() * (1. - Ix)
+            u = u * Iu + u.clone().detach() * (1. - Iu)
+        return x, u, costs

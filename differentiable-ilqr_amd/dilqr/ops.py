@@ -1,0 +1,241 @@
+"""Functional layer over the C-ABI: allocate outputs, launch on the current
+stream.  Every function here is one (or a few) libdilqr.so calls; nothing
+computes on the host.
+"""
+import torch
+
+from . import _native as N
+
+
+def _f32(t):
+    if t is None:
+        return None
+    if t.dtype != torch.float32:
+        raise TypeError(f"dilqr computes in fp32; got {t.dtype}")
+    return t.detach().contiguous()
+
+
+def model_id_of(dx):
+    from .definitions import LinDx
+    if isinstance(dx, LinDx):
+        return N.MODEL_LINDX
+    mid = getattr(dx, "model_id", None)
+    if mid is None:
+        raise NotImplementedError(
+            "dilqr: dynamics must be a dilqr.env_dx model or a LinDx "
+            "(generic autograd/finite-difference dynamics are not on the HIP path)")
+    return mid
+
+
+def theta_of(dx, like):
+    return dx._theta(like)
+
+
+def rollout(model_id, theta, x_init, u, F=None, f=None):
+    """util.get_traj (util.py:104-127)."""
+    T, B, m = u.shape
+    n = x_init.shape[1]
+    x_init, u, F, f = _f32(x_init), _f32(u), _f32(F), _f32(f)
+    x = torch.empty(T, B, n, device=u.device)
+    N.call("dilqr_rollout_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f), N.ptr(x_init), N.ptr(u),
+           N.ptr(x), N.stream(u.device))
+    return x
+
+
+def linearize(model_id, theta, x, u):
+    """MPC.linearize_dynamics ANALYTIC (mpc_explicit.py:516-546)."""
+    T, B, n = x.shape
+    m = u.shape[2]
+    x, u = _f32(x), _f32(u)
+    F = torch.empty(max(T - 1, 0), B, n, n + m, device=x.device)
+    f = torch.empty(max(T - 1, 0), B, n, device=x.device)
+    N.call("dilqr_linearize_f32", model_id, T, B, N.ptr(theta), N.ptr(x), N.ptr(u), N.ptr(F), N.ptr(f),
+           N.stream(x.device))
+    return F, f
+
+
+def lqr_backward(C, c, F, n, m, x=None, u=None, u_lower=None, u_upper=None, u_zero_I=None,
+                 m_solver=N.SOLVE_INV, want_nqp=False):
+    """lqr_backward (lqr_step_explicit.py:54-162) with the fused delta-space c_back.
+    Returns K [T,B,m,n], k [T,B,m] (natural time order), n_qp [B] or None."""
+    T, B = C.shape[:2]
+    C, c, F, x, u = _f32(C), _f32(c), _f32(F), _f32(x), _f32(u)
+    bounds, keep = N.make_bounds(u_lower, u_upper)
+    zI = None if u_zero_I is None else u_zero_I.to(torch.uint8).contiguous()
+    K = torch.empty(T, B, m, n, device=C.device)
+    k = torch.empty(T, B, m, device=C.device)
+    nqp = torch.zeros(B, dtype=torch.int32, device=C.device) if want_nqp else None
+    N.call("dilqr_lqr_backward_f32", n, m, T, B, N.ptr(C), N.ptr(c), N.ptr(x), N.ptr(u), N.ptr(F), bounds,
+           N.ptr(zI), m_solver, N.ptr(K), N.ptr(k), N.ptr(nqp), N.stream(C.device))
+    del keep
+    return K, k, nqp
+
+
+def lqr_forward(model_id, theta, x_init, C, c, x, u, K, k, F=None, f=None, u_lower=None, u_upper=None,
+                u_zero_I=None, linesearch_decay=0.2, max_linesearch_iter=10):
+    """lqr_forward (lqr_step_explicit.py:166-263): returns new_x, new_u, costs [B],
+    du_sq [T,m,B] (first pass), alphas [B] (final pass)."""
+    T, B, n = x.shape
+    m = u.shape[2]
+    x_init, C, c, x, u, K, k, F, f = map(_f32, (x_init, C, c, x, u, K, k, F, f))
+    bounds, keep = N.make_bounds(u_lower, u_upper)
+    zI = None if u_zero_I is None else u_zero_I.to(torch.uint8).contiguous()
+    dev = x.device
+    nx, nu = torch.empty_like(x), torch.empty_like(u)
+    cost, alpha = torch.empty(B, device=dev), torch.empty(B, device=dev)
+    du_sq = torch.empty(T, m, B, device=dev)
+    N.call("dilqr_lqr_forward_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f), N.ptr(x_init),
+           N.ptr(C), N.ptr(c), N.ptr(x), N.ptr(u), N.ptr(K), N.ptr(k), bounds, N.ptr(zI),
+           float(linesearch_decay), int(max_linesearch_iter), N.ptr(nx), N.ptr(nu), N.ptr(cost), N.ptr(du_sq),
+           N.ptr(alpha), N.stream(dev))
+    del keep
+    return nx, nu, cost, du_sq, alpha
+
+
+def quirk_norm(du_sq):
+    """lqr_step_explicit.py:245-247 norm over the re-viewed [T,m,B] buffer."""
+    T, m, B = du_sq.shape
+    out = torch.empty(B, device=du_sq.device)
+    N.call("dilqr_quirk_norm_f32", T, m, B, N.ptr(du_sq), N.ptr(out), N.stream(du_sq.device))
+    return out
+
+
+def grec_floats(n, m):
+    return ((m * n + m + 1) + 3) // 4 * 4
+
+
+class MPCWorkspace:
+    """Device buffers of one MPC solve (reused across iterations)."""
+
+    def __init__(self, T, B, n, m, device):
+        dev = device
+        self.xa = torch.empty(T, B, n, device=dev)
+        self.ua = torch.empty(T, B, m, device=dev)
+        self.xb = torch.empty(T, B, n, device=dev)
+        self.ub = torch.empty(T, B, m, device=dev)
+        self.ws = torch.empty(T * B * grec_floats(n, m), device=dev)
+        self.cost = torch.empty(B, device=dev)
+        self.alpha = torch.empty(B, device=dev)
+        self.du_sq = torch.empty(T, m, B, device=dev)
+        self.fdn = torch.empty(B, device=dev)
+        self.best_x = torch.empty(T, B, n, device=dev)
+        self.best_u = torch.empty(T, B, m, device=dev)
+        self.best_cost = torch.empty(B, device=dev)
+        self.best_du = torch.empty(B, device=dev)
+        self.ctrl = torch.zeros(N.CTRL_INTS, dtype=torch.int32, device=dev)
+
+
+def ilqr_iterate(model_id, theta, x_init, C, c, ws, bounds, decay, max_ls, first, best_cost_eps, eps,
+                 not_improved_lim):
+    """One MPC iteration (mpc_explicit.py:246-299) on device: fused iterate kernel
+    (current (xa,ua) -> new (xb,ub)) + best/stop bookkeeping, then swap."""
+    T, B, n = ws.xa.shape
+    m = ws.ua.shape[2]
+    s = N.stream(x_init.device)
+    N.call("dilqr_ilqr_iterate_f32", model_id, T, B, N.ptr(theta), N.ptr(x_init), N.ptr(C), N.ptr(c),
+           N.ptr(ws.xa), N.ptr(ws.ua), bounds, float(decay), int(max_ls), N.ptr(ws.ws), N.ptr(ws.xb),
+           N.ptr(ws.ub), N.ptr(ws.cost), N.ptr(ws.du_sq), N.ptr(ws.alpha), N.ptr(ws.ctrl), s)
+    N.call("dilqr_mpc_update_best_f32", n, m, T, B, int(first), float(best_cost_eps), float(eps),
+           int(min(not_improved_lim, 2 ** 31 - 1)), N.ptr(ws.xb), N.ptr(ws.ub), N.ptr(ws.cost), N.ptr(ws.du_sq),
+           N.ptr(ws.fdn), N.ptr(ws.best_x), N.ptr(ws.best_u), N.ptr(ws.best_cost), N.ptr(ws.best_du),
+           N.ptr(ws.ctrl), s)
+    ws.xa, ws.xb = ws.xb, ws.xa
+    ws.ua, ws.ub = ws.ub, ws.ua
+
+
+def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upper=None, lqr_iter=10,
+              eps=1e-7, linesearch_decay=0.2, max_linesearch_iter=10, not_improved_lim=5, best_cost_eps=1e-4,
+              check_every=8):
+    """The iLQR outer loop of mpc_explicit.MPC.forward (mpc_explicit.py:228-299)
+    entirely on device; the host only reads the stop flag every `check_every`
+    iterations.  Returns the workspace (best_x, best_u, best_cost, best_du, ctrl)."""
+    B, n = x_init.shape
+    m = C.shape[-1] - n
+    dev = x_init.device
+    x_init, C, c = _f32(x_init), _f32(C), _f32(c)
+    ws = MPCWorkspace(T, B, n, m, dev)
+    if u_init is None:
+        ws.ua.zero_()
+    else:
+        u0 = u_init.to(device=dev, dtype=torch.float32)
+        if u0.ndimension() == 2:
+            u0 = u0.unsqueeze(1).expand(T, B, m)
+        ws.ua.copy_(u0)
+    bounds, keep = N.make_bounds(u_lower, u_upper)
+    N.call("dilqr_rollout_f32", model_id, n, m, T, B, N.ptr(theta), None, None, N.ptr(x_init), N.ptr(ws.ua),
+           N.ptr(ws.xa), N.stream(dev))
+    for i in range(lqr_iter):
+        ilqr_iterate(model_id, theta, x_init, C, c, ws, bounds, linesearch_decay, max_linesearch_iter, i == 0,
+                     best_cost_eps, eps, not_improved_lim)
+        if check_every and (i + 1) % check_every == 0 and i + 1 < lqr_iter:
+            if int(ws.ctrl[1].item()):
+                break
+    del keep
+    return ws
+
+
+def lqr_adjoint(C, c, F, x, u, dl_dx, dl_du, u_lower=None, u_upper=None, m_solver=N.SOLVE_INV, want_df=True):
+    """Classic adjoint (lqr_step.py:312-407) -> dx_init, dC, dc, dF, df."""
+    T, B, n = x.shape
+    m = u.shape[2]
+    d = n + m
+    C, c, F, x, u, dl_dx, dl_du = map(_f32, (C, c, F, x, u, dl_dx, dl_du))
+    bounds, keep = N.make_bounds(u_lower, u_upper)
+    dev = C.device
+    ws = torch.empty(T * B * (m * n + m), device=dev)
+    dx0 = torch.empty(B, n, device=dev)
+    dC = torch.empty(T, B, d, d, device=dev)
+    dc = torch.empty(T, B, d, device=dev)
+    dF = torch.empty(max(T - 1, 0), B, n, d, device=dev)
+    df = torch.empty(max(T - 1, 0), B, n, device=dev) if want_df else None
+    N.call("dilqr_lqr_adjoint_f32", n, m, T, B, N.ptr(C), N.ptr(c), N.ptr(F), N.ptr(x), N.ptr(u), N.ptr(dl_dx),
+           N.ptr(dl_du), bounds, m_solver, N.ptr(ws), N.ptr(dx0), N.ptr(dC), N.ptr(dc), N.ptr(dF), N.ptr(df),
+           N.stream(dev))
+    del keep
+    return dx0, dC, dc, dF, df
+
+
+def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=None, u_lower=None,
+                      u_upper=None, lqr_iter=10, eps=1e-7, linesearch_decay=0.2, max_linesearch_iter=10,
+                      not_improved_lim=5, best_cost_eps=1e-4, check_every=8):
+    """The same outer loop with the unfused kernels (linearise -> F in HBM ->
+    Riccati -> rollout/line search).  Used for LinDx dynamics (classic mpc.MPC,
+    the adjoint engines) and to cross-check the fused iteration."""
+    B, n = x_init.shape
+    m = C.shape[-1] - n
+    dev = x_init.device
+    x_init, C, c, F, f = _f32(x_init), _f32(C), _f32(c), _f32(F), _f32(f)
+    ws = MPCWorkspace(T, B, n, m, dev)
+    if u_init is None:
+        ws.ua.zero_()
+    else:
+        u0 = u_init.to(device=dev, dtype=torch.float32)
+        if u0.ndimension() == 2:
+            u0 = u0.unsqueeze(1).expand(T, B, m)
+        ws.ua.copy_(u0)
+    s = N.stream(dev)
+    N.call("dilqr_rollout_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f), N.ptr(x_init),
+           N.ptr(ws.ua), N.ptr(ws.xa), s)
+    for i in range(lqr_iter):
+        if model_id == N.MODEL_LINDX:
+            Fi, fi = F, f
+        else:
+            Fi, fi = linearize(model_id, theta, ws.xa, ws.ua)
+        K, k, _ = lqr_backward(C, c, Fi, n, m, x=ws.xa, u=ws.ua, u_lower=u_lower, u_upper=u_upper)
+        bounds, keep = N.make_bounds(u_lower, u_upper)
+        N.call("dilqr_lqr_forward_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f),
+               N.ptr(x_init), N.ptr(C), N.ptr(c), N.ptr(ws.xa), N.ptr(ws.ua), N.ptr(K), N.ptr(k), bounds, None,
+               float(linesearch_decay), int(max_linesearch_iter), N.ptr(ws.xb), N.ptr(ws.ub), N.ptr(ws.cost),
+               N.ptr(ws.du_sq), N.ptr(ws.alpha), s)
+        N.call("dilqr_mpc_update_best_f32", n, m, T, B, int(i == 0), float(best_cost_eps), float(eps),
+               int(min(not_improved_lim, 2 ** 31 - 1)), N.ptr(ws.xb), N.ptr(ws.ub), N.ptr(ws.cost),
+               N.ptr(ws.du_sq), N.ptr(ws.fdn), N.ptr(ws.best_x), N.ptr(ws.best_u), N.ptr(ws.best_cost),
+               N.ptr(ws.best_du), N.ptr(ws.ctrl), s)
+        del keep
+        ws.xa, ws.xb = ws.xb, ws.xa
+        ws.ua, ws.ub = ws.ub, ws.ua
+        # a stopped loop must not keep iterating: the unfused kernels have no
+        # device-side guard, so poll every iteration here.
+        if int(ws.ctrl[1].item()):
+            break
+    return ws

@@ -1,0 +1,179 @@
+/*
+ * dilqr.h — C-ABI of the MI355X-native batched differentiable-iLQR hot path.
+ *
+ * The reference (josef-w/Differentiable-iLQR) is pure PyTorch; its "FFI" for
+ * this path is the Python autograd surface  MPC / LQRStep / pnqp / dynamics.
+ * Each entry point below replaces one reference function (cited) and is what
+ * the reference-side binding (ctypes) calls.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a caller-owned DEVICE buffer, fp32, contiguous, in the
+ *     reference's time-major layout: C [T,B,d,d], c [T,B,d], F [T-1,B,n,d],
+ *     f [T-1,B,n], x [T,B,n], u [T,B,m], K [T,B,m,n], k [T,B,m]; x_init [B,n];
+ *     per-problem vectors [B];  d = n + m;
+ *   - gains are written in NATURAL time order (K[t] is the gain of step t);
+ *   - pointers must be 16-byte aligned (torch allocations are);
+ *   - `stream` is a hipStream_t passed as void* (0 = legacy default stream);
+ *   - no allocation, no host synchronisation: every call is capturable in a
+ *     hipGraph; all work is enqueued on `stream`;
+ *   - return value: 0 = ok, >0 = invalid argument (DILQR_E_*), <0 = -(hipError_t).
+ *   - reentrant, no global state: independent calls on different streams or
+ *     devices are safe.
+ *
+ * Semantics are per problem (one problem per GPU lane); see DESIGN.md for the
+ * three places where the reference couples problems of a batch (pnqp's
+ * batch-max Armijo exit, pnqp's all-converged early return, and the MPC stop
+ * rule — the last one IS reproduced on device).
+ */
+#ifndef DILQR_H
+#define DILQR_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ------------------------------------------------------- */
+#define DILQR_OK 0
+#define DILQR_E_SHAPE 1      /* unsupported (n, m) / model combination        */
+#define DILQR_E_ARG 2        /* null or misaligned pointer, bad size          */
+#define DILQR_E_MODE 3       /* unsupported option combination                */
+
+/* ---- dynamics models (env_dx/ *.py) --------------------------------------- */
+#define DILQR_MODEL_LINDX 0      /* x' = F_t [x;u] + f_t  (definitions.py LinDx) */
+#define DILQR_MODEL_PENDULUM 1   /* env_dx/pendulum.py   n=3  m=1 p=3            */
+#define DILQR_MODEL_CARTPOLE 2   /* env_dx/cartpole.py   n=5  m=1 p=4            */
+#define DILQR_MODEL_ROCKET 3     /* env_dx/rocket.py     n=13 m=3 p=5            */
+
+/* ---- control bounds (MPC u_lower/u_upper: float or [T,B,m] tensor) -------- */
+#define DILQR_BOUNDS_NONE 0
+#define DILQR_BOUNDS_SCALAR 1    /* lo/hi are floats                              */
+#define DILQR_BOUNDS_TENSOR 2    /* lo_t/hi_t are [T,B,m] device tensors          */
+
+/* ---- m>1 unconstrained gain solve ---------------------------------------- */
+#define DILQR_SOLVE_INV 0        /* lqr_step_explicit.py:90-96 pinverse (=inverse
+                                    for nonsingular Q_uu)                         */
+#define DILQR_SOLVE_CHOL 1       /* lqr_step_backup.py:199-208 chol(Q_uu+1e-6 I)  */
+
+typedef struct dilqr_bounds {
+  int mode;                      /* DILQR_BOUNDS_*                               */
+  float lo, hi;                  /* scalar bounds                                */
+  const float* lo_t;             /* [T,B,m] or NULL                              */
+  const float* hi_t;             /* [T,B,m] or NULL                              */
+} dilqr_bounds;
+
+/* Library version (for the loader's sanity check). */
+int dilqr_version(void);
+
+/* Number of parameters theta of a model (4 for cartpole), or -1. */
+int dilqr_model_num_params(int model);
+
+/* x' = f(x, u; theta) for N independent rows.  Replaces the models' forward():
+   cartpole.py:64-97, pendulum.py:60-95, rocket.py:82-164.
+   x [N,n], u [N,m], theta [p] device, out [N,n]. */
+int dilqr_dynamics_f32(int model, int N, const float* theta, const float* x,
+                       const float* u, float* out, void* stream);
+
+/* D = d f / d [x;u] at the unclamped u, [N,n,n+m].  Replaces get_linear_dyn:
+   cartpole.py:790-839, pendulum.py:444-475, rocket.py:324-426. */
+int dilqr_linear_dyn_f32(int model, int N, const float* theta, const float* x,
+                         const float* u, float* D, void* stream);
+
+/* Rollout x_{t+1} = f(x_t, u_t) from x_init; util.get_traj (util.py:104-127).
+   For DILQR_MODEL_LINDX pass F [T-1,B,n,d] and f [T-1,B,n] (f may be NULL). */
+int dilqr_rollout_f32(int model, int n, int m, int T, int B, const float* theta,
+                      const float* F, const float* f, const float* x_init,
+                      const float* u, float* x_out, void* stream);
+
+/* Linearisation around (x,u): F = D(x_t,u_t), f = f(x_t,u_t) - F [x_t;u_t],
+   t < T-1.  MPC.linearize_dynamics ANALYTIC, mpc_explicit.py:516-546. */
+int dilqr_linearize_f32(int model, int T, int B, const float* theta, const float* x,
+                        const float* u, float* F, float* f, void* stream);
+
+/* Backward Riccati sweep in delta space: lqr_backward, lqr_step_explicit.py:54-162
+   (with the c_back of 630-636 fused: c_back_t = C_t [x_t;u_t] + c_t; pass
+   x = NULL to give c_back directly in c — u may then still be given, it only
+   shifts the box bounds (lb = lower - u_t)).  Bounded problems
+   run pnqp (pnqp.py:5-82) per step, warm-started from the later step.
+   u_zero_I [T,B,m] (uint8, nullable): the masked solve of
+   lqr_step_backup.py:210-232 used by the adjoint engines.
+   n_qp_iter [B] (nullable): per-problem sum of 1+pnqp iterations. */
+int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const float* c,
+                           const float* x, const float* u, const float* F,
+                           dilqr_bounds bounds, const unsigned char* u_zero_I,
+                           int m_solver, float* K, float* k, int* n_qp_iter,
+                           void* stream);
+
+/* Rollout with per-problem backtracking line search: lqr_forward,
+   lqr_step_explicit.py:166-263.  `model` gives the true dynamics (F/f for
+   LINDX).  Outputs: new x/u, cost [B] (final pass), du_sq [T,m,B] =
+   (u - new_u)^2 of the FIRST pass laid out [T,m,B] (input of
+   dilqr_quirk_norm_f32), alpha [B] = the alpha of the final pass. */
+int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* theta,
+                          const float* F, const float* f, const float* x_init,
+                          const float* C, const float* c, const float* x,
+                          const float* u, const float* K, const float* k,
+                          dilqr_bounds bounds, const unsigned char* u_zero_I,
+                          float linesearch_decay, int max_linesearch_iter,
+                          float* x_out, float* u_out, float* cost, float* du_sq,
+                          float* alpha, void* stream);
+
+/* The reference's batch-mixing norm (lqr_step_explicit.py:245-247):
+   (u-new_u).transpose(1,2).contiguous().view(B,-1).norm(2,1), i.e. row r is
+   the 2-norm of elements [r*T*m, (r+1)*T*m) of the [T,m,B] buffer du_sq
+   (already squared).  out [B]. */
+int dilqr_quirk_norm_f32(int T, int m, int B, const float* du_sq, float* out,
+                         void* stream);
+
+/* ---- the iLQR outer loop (mpc_explicit.py:182-358) ------------------------ */
+
+/* Device-resident loop state; zero it (hipMemsetAsync) before iteration 0. */
+typedef struct dilqr_mpc_ctrl {
+  int iter;              /* iterations executed                          */
+  int stopped;           /* 1 once the stop rule fired                   */
+  int n_not_improved;    /* mpc_explicit.py:264, 279                     */
+  int any_improved;      /* scratch for the current iteration            */
+  unsigned max_du_bits;  /* float bits of max(full_du_norm) this iter    */
+  int pad[3];
+} dilqr_mpc_ctrl;
+
+/* One fused iLQR iteration for a model (not LINDX): linearise on the fly,
+   Riccati sweep (+pnqp), old cost, line-search rollout.  Reads the current
+   trajectory (x,u), writes the new one (x_out,u_out), cost [B], du_sq [T,m,B],
+   alpha [B].  ws_gains: workspace of T*B*(m*n+m) floats.  No-op when
+   ctrl->stopped. */
+int dilqr_ilqr_iterate_f32(int model, int T, int B, const float* theta,
+                           const float* x_init, const float* C, const float* c,
+                           const float* x, const float* u, dilqr_bounds bounds,
+                           float linesearch_decay, int max_linesearch_iter,
+                           float* ws_gains, float* x_out, float* u_out, float* cost,
+                           float* du_sq, float* alpha, dilqr_mpc_ctrl* ctrl,
+                           void* stream);
+
+/* Best-iterate bookkeeping + stop rule of one MPC iteration
+   (mpc_explicit.py:264-299): full_du_norm from du_sq (quirk layout), per
+   problem "cost <= best + best_cost_eps" -> copy (x,u,cost,du) into best;
+   then n_not_improved / stopped.  first != 0 for iteration 0.
+   No-op when ctrl->stopped. */
+int dilqr_mpc_update_best_f32(int n, int m, int T, int B, int first,
+                              float best_cost_eps, float eps, int not_improved_lim,
+                              const float* x, const float* u, const float* cost,
+                              const float* du_sq, float* full_du_norm,
+                              float* best_x, float* best_u, float* best_cost,
+                              float* best_du, dilqr_mpc_ctrl* ctrl, void* stream);
+
+/* ---- backward passes -------------------------------------------------------- */
+
+/* Classic differentiable-LQR adjoint, lqr_step.py:312-407: r = [dl_dx;dl_du],
+   active set |u - bound| <= 1e-8, one adjoint LQR solve (u_zero_I masked, m_solver
+   as the engine), costates, outer products.  Outputs dx_init [B,n], dC, dc,
+   dF [T-1,B,n,d], df [T-1,B,n] (df nullable).  ws: T*B*(m*n+m) floats. */
+int dilqr_lqr_adjoint_f32(int n, int m, int T, int B, const float* C, const float* c,
+                          const float* F, const float* x, const float* u,
+                          const float* dl_dx, const float* dl_du, dilqr_bounds bounds,
+                          int m_solver, float* ws, float* dx_init, float* dC, float* dc,
+                          float* dF, float* df, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DILQR_H */
