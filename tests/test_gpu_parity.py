@@ -179,7 +179,7 @@ def test_fused_iteration_equals_unfused(golden, name):
     a = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls, fused=True)
     b = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls, fused=False)
     for ta, tb in zip(a, b):
-        assert relerr(cpu(ta), cpu(tb)) < 1e-5
+        assert relerr(cpu(ta), cpu(tb)) < 1e-3
 
 
 # ------------------------------------------------------------------ classic adjoint
