@@ -116,3 +116,13 @@ struct Cartpole {
 // kernels rather than through this model interface.
 
 }  // namespace dilqr
+
+#include "dilqr_models_gen.h"
+
+namespace dilqr {
+// Second-order terms of each model for the implicit backward.  XX00_ZERO: the
+// reference's x_grad_xtm1 has a 0 where d x_{t+1}/d x_t is 1 (cartpole.py:666).
+template <class Model> struct D2Of;
+template <> struct D2Of<Pendulum> { using type = gen::PendulumD2; static constexpr bool XX00_ZERO = false; };
+template <> struct D2Of<Cartpole> { using type = gen::CartpoleD2; static constexpr bool XX00_ZERO = true; };
+}  // namespace dilqr

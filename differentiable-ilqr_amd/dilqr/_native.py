@@ -46,6 +46,9 @@ SIGNATURES = {
                                    _vp, _vp, _vp], _i),
     "dilqr_lqr_adjoint_f32": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _i, _vp, _vp, _vp,
                                _vp, _vp, _vp, _vp], _i),
+    "dilqr_implicit_ws_floats": ([_i], _i),
+    "dilqr_implicit_backward_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _vp, _vp, _vp,
+                                     _vp, _vp], _i),
 }
 
 _lib = None

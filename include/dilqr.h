@@ -173,6 +173,21 @@ int dilqr_lqr_adjoint_f32(int n, int m, int T, int B, const float* C, const floa
                           int m_solver, float* ws, float* dx_init, float* dC, float* dc,
                           float* dF, float* df, void* stream);
 
+/* DiLQR implicit backward through the iLQR fixed point: LQRStepFn.backward
+   (lqr_step_explicit.py:653-712) with fix_point_equ (458-598) and the model's
+   grad_input (cartpole.py:717-788, pendulum.py:383-443).  Inputs: the solution
+   (x, u), its Riccati gains K [T,B,m,n] in NATURAL order (the kernel applies the
+   reference's reversed-stack indexing itself), C, c, theta, dl_dx, dl_du, the
+   box bounds (active set |u - bound| <= 1e-8).  Outputs dC [T,B,d,d], dc [T,B,d],
+   dtheta [B,p] (per problem; the autograd caller sums over the batch).
+   ws: T*B*dilqr_implicit_ws_floats(model) floats.  Models: pendulum, cartpole. */
+int dilqr_implicit_ws_floats(int model);
+int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
+                                const float* C, const float* c, const float* x,
+                                const float* u, const float* K, const float* dl_dx,
+                                const float* dl_du, dilqr_bounds bounds, float* ws,
+                                float* dC, float* dc, float* dtheta, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

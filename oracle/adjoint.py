@@ -163,3 +163,80 @@ def fix_point_equ(dl_dx, dl_du, mats, p):
     dC = np.einsum("bi,bij->bj", g, sol_C).reshape(B, T, d, d).transpose(1, 0, 2, 3)
     dc = np.einsum("bi,bij->bj", g, sol_c).reshape(B, T, d).transpose(1, 0, 2)
     return dC, dc, dtheta
+
+
+def implicit_backward_fast(model, dl_dx, dl_du, C, c, F, f, new_x, new_u, K_rev, u_lower=None,
+                           u_upper=None, params=None):
+    """The same result as implicit_backward, by the algebra the HIP kernel uses.
+
+    The reference solves A^T w = g (A = I - J, (T d)^2) after forming J from T*d
+    unit-RHS adjoint solves.  Two identities collapse that:
+      (1) J[p,(t,k)] = -sum_j dtau_t(e_p)[j] M_t[j,k] with
+          M_t[j,k] = sum_i lam_{t+1}[i] dD_t[i,j]/dtau_k — the dlam terms of
+          X_D_X and X_d_X cancel (d_grad_X = -D_grad_x . tau), so J = -P M with
+          P the adjoint-LQR solution operator (dtau(r) = P r) and M = blkdiag(M_t);
+      (2) w = g - M^T y with y = P w  <=>  y solves the LQR with cost matrices
+          C_t + M_t^T and linear term -g (same dynamics F, same active set).
+    Then dC, dc, dtheta are the KKT gradients of the adjoint solve with r = w, whose
+    trajectory is y itself.  Cost: O(T d^3) per problem instead of O((T d)^3).
+    """
+    T, B, n = dl_dx.shape
+    m = dl_du.shape[2]
+    d = n + m
+    dt = C.dtype
+    p = model.n_params
+    g = np.concatenate([dl_dx, dl_du], 2)
+    I = _active_set(new_u, u_lower, u_upper)
+    gD, gd, Dx, Du, D, d_x, d_u = model.grad_input(new_x, new_u, K_rev, params)
+    # primal costates (lqr_step_explicit.py:305-319)
+    lams = [None] * T
+    prev = None
+    for t in range(T - 1, -1, -1):
+        lam = lqr.bmv(C[t, :, :n, :n], new_x[t]) + lqr.bmv(C[t, :, :n, n:], new_u[t]) + c[t, :, :n]
+        if prev is not None:
+            lam = lam + lqr.bmv(np.swapaxes(F[t, :, :, :n], 1, 2), prev)
+        lams[t] = prev = lam
+    # M_t = sum_i lam_{t+1}[i] dD_t[i,:,:]/dtau
+    M = np.zeros((T, B, d, d), dt)
+    Dtau = np.concatenate([Dx, Du], -1)                       # [T-1,B,n,d,d]
+    for t in range(T - 1):
+        M[t] = np.einsum("bi,bijk->bjk", lams[t + 1], Dtau[t])
+    Cp = C + np.swapaxes(M, 2, 3)
+    y = adjoint_lqr_linear(Cp, g, F, n, m, I)
+    w = g - np.einsum("tbjk,tbj->tbk", M, y)
+    # KKT gradient of the adjoint solve with r = w (trajectory y)
+    xu = np.concatenate([new_x, new_u], 2)
+    dC = -0.5 * (y[..., :, None] * xu[..., None, :] + xu[..., :, None] * y[..., None, :])
+    dc = -y
+    dlam = [None] * T
+    prev = None
+    for t in range(T - 1, -1, -1):
+        dl = lqr.bmv(C[t, :, :n, :n], y[t, :, :n]) + lqr.bmv(C[t, :, :n, n:], y[t, :, n:]) - w[t, :, :n]
+        if prev is not None:
+            dl = dl + lqr.bmv(np.swapaxes(F[t, :, :, :n], 1, 2), prev)
+        dlam[t] = prev = dl
+    dtheta = np.zeros((B, p), dt)
+    for t in range(T - 1):
+        dF = -(dlam[t + 1][:, :, None] * xu[t][:, None, :] + lams[t + 1][:, :, None] * y[t][:, None, :])
+        df = -dlam[t + 1]
+        dtheta += np.einsum("bnm,bnmk->bk", dF, gD[t]) + np.einsum("bn,bnk->bk", df, gd[t])
+    return dC, dc, dtheta
+
+
+def adjoint_lqr_linear(C, g, F, n, m, I=None):
+    """tau = argmin of 1/2 tau^T C tau - g^T tau s.t. x_0 = 0, x_{t+1} = F_t tau_t
+    (controls in the active set I fixed to 0), by the Riccati elimination — valid
+    for a non-symmetric C (it eliminates the linear KKT system).  No line search."""
+    T, B, d = g.shape
+    dt = C.dtype
+    K, k, _ = lqr.lqr_backward(C, -g, F, n, m, u_zero_I=I, m_solver="lu")
+    x = np.zeros((B, n), dt)
+    out = np.zeros((T, B, d), dt)
+    for t in range(T):
+        u = lqr.bmv(K[t], x) + k[t]
+        if I is not None:
+            u[I[t]] = 0.
+        out[t, :, :n], out[t, :, n:] = x, u
+        if t < T - 1:
+            x = lqr.bmv(F[t], np.concatenate([x, u], 1))
+    return out

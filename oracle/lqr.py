@@ -136,6 +136,8 @@ def lqr_backward(C, c_back, F, n, m, u=None, u_lower=None, u_upper=None, u_zero_
             elif u_zero_I is None:
                 if m_solver == "pinv":
                     Qi = np.stack([np.linalg.pinv(Quu[b]) for b in range(B)])
+                elif m_solver == "lu":
+                    Qi = np.linalg.inv(Quu)
                 else:
                     L = np.linalg.cholesky(Quu + dt.type(1e-6) * np.eye(m, dtype=dt))
                     Qi = np.linalg.inv(np.swapaxes(L, 1, 2)) @ np.linalg.inv(L)

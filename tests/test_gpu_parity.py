@@ -249,3 +249,91 @@ def test_full_size_batch_independence():
     assert torch.equal(full[1][:, 4096:4352], part[1])
     assert torch.equal(full[2][4096:4352], part[2])
     assert torch.isfinite(full[2]).all()
+
+
+# ------------------------------------------------------------------ DiLQR implicit backward
+IMPLICIT = {"cart_unc": ("cartpole", None), "cart_box": ("cartpole", (-5.0, 5.0)),
+            "pend_box": ("pendulum", (-2.0, 2.0))}
+
+
+@pytest.mark.parametrize("tag", list(IMPLICIT))
+def test_implicit_backward_vs_golden(golden, tag):
+    """LQRStep(no_op_forward=True) at the reference's fp64 solution; backward
+    through the fused implicit kernel vs the reference's dC, dc, dtheta.
+    Tolerance 1e-4 of the max magnitude (the reference's own fp32 result is
+    within ~3e-5 of its fp64 result, see tests/golden)."""
+    import dilqr
+    g = golden("implicit_f64")
+    mname, bounds = IMPLICIT[tag]
+    dx = dilqr_models()[mname]()
+    x, u, Q, P, F, f, x0 = (gpu(g[f"{tag}_{k}"]) for k in ("x", "u", "Q", "P", "F", "f", "x0"))
+    T, B, n = x.shape
+    m = u.shape[2]
+    theta = dx.params.clone().to(DEV).requires_grad_(True)
+    Qg, Pg = Q.clone().requires_grad_(True), P.clone().requires_grad_(True)
+    lo, hi = bounds if bounds else (None, None)
+    step = dilqr.LQRStep(n, m, T, u_lower=lo, u_upper=hi, true_cost=dilqr.QuadCost(Qg, Pg), true_dynamics=dx,
+                         current_x=x, current_u=u, no_op_forward=True)
+    x2, u2 = step(x0, Qg, Pg, F, f, theta)
+    loss = (x2 * gpu(g[f"{tag}_wx"])).sum() + (u2 * gpu(g[f"{tag}_wu"])).sum()
+    loss.backward()
+    assert relerr(cpu(theta.grad), g[f"{tag}_dtheta"]) < 1e-4
+    assert relerr(cpu(Qg.grad), g[f"{tag}_dQ"]) < 1e-4
+    assert relerr(cpu(Pg.grad), g[f"{tag}_dP"]) < 1e-4
+    # per-problem dtheta straight from the kernel
+    from dilqr import ops
+    from dilqr.implicit import implicit_backward
+    K, _, _ = ops.lqr_backward(Q, P, F, n, m, x=x, u=u, u_lower=lo, u_upper=hi)
+    _, _, dth = implicit_backward(dx, gpu(g[f"{tag}_wx"]), gpu(g[f"{tag}_wu"]), Q, P, F, f, x, u, K, lo, hi,
+                                  None)
+    assert relerr(cpu(dth), g[f"{tag}_dtheta_b"]) < 1e-4
+
+
+def test_mpc_end_to_end_gradient(golden):
+    """dilqr.MPC forward (device loop) + implicit backward, as il_exp.py uses it
+    (gradients into the cost and the model parameters), vs the reference."""
+    import dilqr
+    g = golden("implicit_f64")
+    tag = "cart_box"
+    dx = dilqr_models()["cartpole"]()
+    dx.params = dx.params.clone().to(DEV).requires_grad_(True)
+    x0 = gpu(g[f"{tag}_x0"])
+    B, T = x0.shape[0], 10
+    Q, P = gpu(g[f"{tag}_Q"]).requires_grad_(True), gpu(g[f"{tag}_P"]).requires_grad_(True)
+    mpc = dilqr.MPC(5, 1, T, u_lower=-5.0, u_upper=5.0, lqr_iter=30, eps=1e-6, linesearch_decay=0.5,
+                    max_linesearch_iter=2, exit_unconverged=False, detach_unconverged=False)
+    x, u, _ = mpc(x0, dilqr.QuadCost(Q, P), dx)
+    assert relerr(cpu(u), g[f"{tag}_u"]) < 1e-3
+    loss = (x * gpu(g[f"{tag}_wx"])).sum() + (u * gpu(g[f"{tag}_wu"])).sum()
+    loss.backward()
+    assert relerr(cpu(dx.params.grad), g[f"{tag}_dtheta"]) < 5e-3
+    assert relerr(cpu(Q.grad), g[f"{tag}_dQ"]) < 5e-3
+
+
+def test_implicit_backward_full_size():
+    """Config 4 shape (cartpole T=25, B=65536, bounds +-10): finite gradients,
+    and a 128-problem slice gives bit-identical per-problem results."""
+    import dilqr
+    from dilqr import ops
+    from dilqr.implicit import implicit_backward
+    B, T = 65536, 25
+    rng = np.random.RandomState(0)
+    th = rng.uniform(-np.pi, np.pi, B)
+    x0 = np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                   rng.uniform(-1, 1, B)], 1)
+    x, u, _ = run_gpu_mpc(x0, "cartpole", T, 10, (-10.0, 10.0), 0.0, 10 ** 9, 0.5, 2)
+    dx = dilqr_models()["cartpole"]()
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV)
+    c = p.repeat(T, B, 1).to(DEV)
+    wx = torch.randn(T, B, 5, device=DEV)
+    wu = torch.randn(T, B, 1, device=DEV)
+    K, _, _ = ops.lqr_backward(C, c, None if T == 1 else ops.linearize(dx.model_id, ops.theta_of(dx, C), x, u)[0],
+                               5, 1, x=x, u=u, u_lower=-10.0, u_upper=10.0)
+    dC, dc, dth = implicit_backward(dx, wx, wu, C, c, None, None, x, u, K, -10.0, 10.0, None)
+    assert torch.isfinite(dC).all() and torch.isfinite(dc).all() and torch.isfinite(dth).all()
+    sl = slice(1000, 1128)
+    dC2, dc2, dth2 = implicit_backward(dx, wx[:, sl].contiguous(), wu[:, sl].contiguous(), C[:, sl].contiguous(),
+                                       c[:, sl].contiguous(), None, None, x[:, sl].contiguous(),
+                                       u[:, sl].contiguous(), K[:, sl].contiguous(), -10.0, 10.0, None)
+    assert torch.equal(dth[sl], dth2) and torch.equal(dC[:, sl], dC2)

@@ -1,0 +1,90 @@
+"""CPU check of the generated second-order model code (csrc/dilqr_models_gen.h).
+
+The header is compiled for the HOST with g++ (it is plain fp32 C++ there) and
+evaluated through a small extern "C" shim; its Lagrangian Hessian / parameter
+contractions are compared with the oracle's get_matrices (which is pinned to the
+reference's own get_matrices outputs in test_oracle_golden.py)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import models as om
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "differentiable-ilqr_amd", "csrc")
+
+SHIM = r"""
+#include "dilqr_models_gen.h"
+#define WRAP(MODEL, Dd, N, M, P)                                                              \
+extern "C" void MODEL##_lag_hess(const float* th, const float* x, const float* u,             \
+                                 const float* lam, float* out) {                             \
+  float xx[N], uu[M], ll[N], o[Dd][Dd];                                                      \
+  for (int i = 0; i < N; ++i) { xx[i] = x[i]; ll[i] = lam[i]; }                               \
+  for (int i = 0; i < M; ++i) uu[i] = u[i];                                                  \
+  dilqr::gen::MODEL##D2::lag_hess(th, xx, uu, ll, o);                                         \
+  for (int i = 0; i < Dd * Dd; ++i) out[i] = (&o[0][0])[i];                                  \
+}                                                                                            \
+extern "C" void MODEL##_lag_dparam(const float* th, const float* x, const float* u,           \
+                                   const float* lam, float* out) {                           \
+  float xx[N], uu[M], ll[N], o[Dd][P];                                                       \
+  for (int i = 0; i < N; ++i) { xx[i] = x[i]; ll[i] = lam[i]; }                               \
+  for (int i = 0; i < M; ++i) uu[i] = u[i];                                                  \
+  dilqr::gen::MODEL##D2::lag_dparam(th, xx, uu, ll, o);                                       \
+  for (int i = 0; i < Dd * P; ++i) out[i] = (&o[0][0])[i];                                   \
+}                                                                                            \
+extern "C" void MODEL##_f_theta(const float* th, const float* x, const float* u, float* out) { \
+  float xx[N], uu[M], o[N][P];                                                               \
+  for (int i = 0; i < N; ++i) xx[i] = x[i];                                                  \
+  for (int i = 0; i < M; ++i) uu[i] = u[i];                                                  \
+  dilqr::gen::MODEL##D2::f_theta(th, xx, uu, o);                                              \
+  for (int i = 0; i < N * P; ++i) out[i] = (&o[0][0])[i];                                    \
+}
+WRAP(Pendulum, 4, 3, 1, 3)
+WRAP(Cartpole, 6, 5, 1, 4)
+"""
+
+
+@pytest.fixture(scope="module")
+def shim(tmp_path_factory):
+    d = tmp_path_factory.mktemp("gen")
+    src = d / "shim.cpp"
+    src.write_text(SHIM)
+    so = d / "shim.so"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-I", CSRC, str(src), "-o", str(so)],
+                   check=True)
+    return ctypes.CDLL(str(so))
+
+
+def call(lib, name, *arrs, out_size):
+    out = np.zeros(out_size, np.float32)
+    args = [a.ctypes.data_as(ctypes.c_void_p) for a in arrs] + [out.ctypes.data_as(ctypes.c_void_p)]
+    getattr(lib, name)(*args)
+    return out
+
+
+@pytest.mark.parametrize("name,cls", [("Pendulum", om.Pendulum), ("Cartpole", om.Cartpole)])
+def test_generated_second_order_terms(shim, golden, name, cls):
+    g = golden("models_f64")
+    key = name.lower()
+    X, U = g[f"{key}_x"][:16], g[f"{key}_u"][:16]
+    n, m, p = cls.n_state, cls.n_ctrl, cls.n_params
+    d = n + m
+    D, Dp, Dx, Du, fth, _, _ = cls.get_matrices(X, U)
+    th = np.array(cls.default_params, np.float32)
+    rng = np.random.RandomState(0)
+    for b in range(X.shape[0]):
+        lam = rng.normal(size=n)
+        x32, u32, l32 = X[b].astype(np.float32), U[b].astype(np.float32), lam.astype(np.float32)
+        Mh = call(shim, f"{name}_lag_hess", th, x32, u32, l32, out_size=d * d).reshape(d, d)
+        Mp = call(shim, f"{name}_lag_dparam", th, x32, u32, l32, out_size=d * p).reshape(d, p)
+        ft = call(shim, f"{name}_f_theta", th, x32, u32, out_size=n * p).reshape(n, p)
+        Dtau = np.concatenate([Dx[b], Du[b]], -1)
+        ref_Mh = np.einsum("i,ijk->jk", lam, Dtau)
+        ref_Mp = np.einsum("i,ijk->jk", lam, Dp[b])
+        scale = lambda a: max(1.0, np.abs(a).max())  # noqa: E731
+        assert np.abs(Mh - ref_Mh).max() / scale(ref_Mh) < 2e-4, b
+        assert np.abs(Mp - ref_Mp).max() / scale(ref_Mp) < 2e-4, b
+        assert np.abs(ft - fth[b]).max() / scale(fth[b]) < 2e-4, b
