@@ -1,0 +1,70 @@
+"""Multi-process (world_size 2, gloo, CPU) coverage of the batch-sharded path
+that bench.py runs on N GPUs: shard boundaries, the per-shard problem set, the
+max-over-ranks timing reduction, and that solving each shard independently gives
+the same per-problem result as solving the whole batch (so no collective is
+needed in the data path).  The per-shard solver here is the CPU oracle; on the
+GPU box the same shards go through the HIP library."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, B_per, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from oracle import models as om
+    from oracle import mpc as ompc
+    B_total = B_per * world
+    x0_all, q, p = bench.make_problems(B_total)
+    lo, hi = bench.shard_rows(B_total, world, rank)
+    assert hi - lo == B_per
+    x0 = x0_all[lo:hi].astype(np.float64)
+    T = 6
+    C, c = ompc.expand_cost(np.diag(q).astype(np.float64), p.astype(np.float64), T, B_per)
+    _, u, costs, _ = ompc.mpc_forward(om.Cartpole, x0, C, c, T, lqr_iter=3, eps=0.0, not_improved_lim=10 ** 9,
+                                      linesearch_decay=0.5, max_linesearch_iter=2)
+    np.save(os.path.join(out_dir, f"u_{rank}.npy"), u)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    assert t.item() == float(world)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_solve_matches_whole_batch(tmp_path):
+    world, B_per = 2, 8
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, B_per, str(tmp_path)), nprocs=world, join=True)
+    import bench
+    from oracle import models as om
+    from oracle import mpc as ompc
+    x0_all, q, p = bench.make_problems(B_per * world)
+    T = 6
+    C, c = ompc.expand_cost(np.diag(q).astype(np.float64), p.astype(np.float64), T, B_per * world)
+    _, u_all, _, _ = ompc.mpc_forward(om.Cartpole, x0_all.astype(np.float64), C, c, T, lqr_iter=3, eps=0.0,
+                                      not_improved_lim=10 ** 9, linesearch_decay=0.5, max_linesearch_iter=2)
+    u_sharded = np.concatenate([np.load(tmp_path / f"u_{r}.npy") for r in range(world)], axis=1)
+    np.testing.assert_allclose(u_sharded, u_all, rtol=0, atol=1e-12)
+
+
+def test_shard_rows_cover_batch():
+    import bench
+    for world in (1, 2, 4, 8):
+        rows = [bench.shard_rows(65536 * world, world, r) for r in range(world)]
+        assert rows[0][0] == 0 and rows[-1][1] == 65536 * world
+        assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
