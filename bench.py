@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--lqr-iter", type=int, default=10)
     ap.add_argument("--batch", type=int, default=B_PER_GPU, help="problems per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernels-only", action="store_true",
+                    help="profiling mode: a few launches of the fused iteration and the sweep, no JSON line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,26 +113,22 @@ def main():
     C = torch.diag(torch.tensor(q)).repeat(T_HORIZON, B, 1, 1).to(dev).contiguous()     # materialised per (t,b)
     c = torch.tensor(p).repeat(T_HORIZON, B, 1).to(dev).contiguous()
     theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
-    ws = ops.MPCWorkspace(T_HORIZON, B, N_STATE, N_CTRL, dev)
+    sv = ops.MPCSolve(T_HORIZON, B, N_STATE, N_CTRL, dev)
     bounds, _ = N.make_bounds(None, None)
     stream = torch.cuda.current_stream(dev)
     s = N.stream(dev)
 
-    def start_solve():
-        ws.ua.zero_()
-        ws.ctrl.zero_()
-        N.call("dilqr_rollout_f32", N.MODEL_CARTPOLE, N_STATE, N_CTRL, T_HORIZON, B, N.ptr(theta), None, None,
-               N.ptr(x0), N.ptr(ws.ua), N.ptr(ws.xa), s)
-
     state = {"i": 0}
 
     def step():
-        if state["i"] % args.lqr_iter == 0:
-            start_solve()
-        ops.ilqr_iterate(N.MODEL_CARTPOLE, theta, x0, C, c, ws, bounds, 0.5, 2, state["i"] % args.lqr_iter == 0,
-                         1e-4, 0.0, 10 ** 9)
+        first = state["i"] % args.lqr_iter == 0
+        if first:
+            sv.begin(N.MODEL_CARTPOLE, theta, x0)
+        sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, first, 1e-4, 0.0, 10 ** 9)
         state["i"] += 1
 
+    if args.kernels_only:
+        args.steps, args.warmup, args.no_cpu_baseline = 0, 2, True
     for _ in range(args.warmup):
         step()
     state["i"] = 0
@@ -149,27 +147,31 @@ def main():
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    assert bool(torch.isfinite(ws.best_cost).all()), "non-finite costs"
+    assert bool(torch.isfinite(sv.best_cost).all()), "non-finite costs"
 
     # ---- roofline of the dominant kernel: the fused iteration, timed with
     # events on ITS stream (the current stream, where ops launch it)
     reps = 10
-    start_solve()
+    sv.begin(N.MODEL_CARTPOLE, theta, x0)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    # the fused iteration kernel alone, on the stream it runs on: dilqr_ilqr_iterate_f32 launches the same
+    # per-problem body (ilqr_problem) as the slot-based MPC loop, reading/writing plain trajectory buffers
+    xa, ua = sv.X3[0], sv.U3[0]
+    xb, ub = sv.X3[1], sv.U3[1]
     for r in range(reps):
         ev[r][0].record(stream)
         N.call("dilqr_ilqr_iterate_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C),
-               N.ptr(c), N.ptr(ws.xa), N.ptr(ws.ua), bounds, 0.5, 2, N.ptr(ws.ws), N.ptr(ws.xb), N.ptr(ws.ub),
-               N.ptr(ws.cost), N.ptr(ws.du_sq), N.ptr(ws.alpha), None, s)
+               N.ptr(c), N.ptr(xa), N.ptr(ua), bounds, 0.5, 2, N.ptr(sv.ws), N.ptr(xb), N.ptr(ub),
+               N.ptr(sv.cost), N.ptr(sv.du_sq), N.ptr(sv.alpha), None, s)
         ev[r][1].record(stream)
-        ws.xa, ws.xb = ws.xb, ws.xa
-        ws.ua, ws.ub = ws.ub, ws.ua
+        xa, xb = xb, xa
+        ua, ub = ub, ua
     torch.cuda.synchronize(dev)
     iter_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     iter_bytes = ITER_BYTES_PER_PROBLEM * B
 
     # standalone Riccati sweep (the north-star's >=50% HBM target kernel)
-    F, _f = ops.linearize(N.MODEL_CARTPOLE, theta, ws.xa, ws.ua)
+    F, _f = ops.linearize(N.MODEL_CARTPOLE, theta, xa, ua)
     K = torch.empty(T_HORIZON, B, N_CTRL, N_STATE, device=dev)
     k = torch.empty(T_HORIZON, B, N_CTRL, device=dev)
     cb = torch.randn(T_HORIZON, B, D, device=dev)
@@ -192,7 +194,9 @@ def main():
         except Exception:
             traffic = None
 
-    if rank == 0:
+    if rank == 0 and args.kernels_only:
+        print(json.dumps({"iter_ms": iter_ms, "sweep_ms": sweep_ms}), flush=True)
+    elif rank == 0:
         value = B_total * args.steps / elapsed
         achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
         sweep_gbs = sweep_bytes / (sweep_ms * 1e-3) / 1e9

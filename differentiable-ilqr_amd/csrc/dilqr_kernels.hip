@@ -370,10 +370,157 @@ __global__ void __launch_bounds__(kBlock) k_quirk_norm(int TM, int B, const floa
 }
 
 // ============================================================ fused iLQR iteration
-// One MPC iteration body (mpc_explicit.py:249-263) for a model: linearise at the
-// current trajectory on the fly, Riccati sweep (+pnqp), the current cost, and
-// the line-search rollout.  F never touches HBM; K/k/obj_t go to a per-lane
-// record that is re-read (L2-hot) by the rollout.
+// One MPC iteration body (mpc_explicit.py:249-263) for ONE problem (this lane):
+// linearise at the current trajectory on the fly, Riccati sweep (+pnqp), the
+// current cost, and the line-search rollout.  F never touches HBM; K/k/obj_t go
+// to a per-lane record that the rollout re-reads (L2/MALL-hot).
+//
+// Latency: at B=65536 there is one wave per SIMD, so every loop software-
+// pipelines its HBM loads one step ahead in registers (the step t-1 / t+1
+// record is in flight while step t computes).
+template <int n, int m>
+struct SweepIn {
+  static constexpr int d = n + m;
+  float C[d][d], c[d], x[n], u[m];
+  DEV void load(const float* __restrict__ Cp, const float* __restrict__ cp, const float* __restrict__ xp,
+                const float* __restrict__ up, size_t tb) {
+    ld2(C, Cp + tb * d * d); ld(c, cp + tb * d); ld(x, xp + tb * n); ld(u, up + tb * m);
+  }
+};
+
+template <int n, int m, int GREC>
+struct FwdIn {
+  static constexpr int d = n + m;
+  float g[GREC], u[m], C[d][d], c[d], xnext[n];
+  DEV void load(const float* __restrict__ grec, const float* __restrict__ up, const float* __restrict__ Cp,
+                const float* __restrict__ cp, const float* __restrict__ xp, size_t tb, size_t tb1) {
+    ld(g, grec + tb * GREC); ld(u, up + tb * m); ld2(C, Cp + tb * d * d); ld(c, cp + tb * d);
+    ld(xnext, xp + tb1 * n);
+  }
+};
+
+template <class Model, int MODE>
+DEV void ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
+                      const float* __restrict__ C, const float* __restrict__ c, const float* __restrict__ x,
+                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
+                      float* __restrict__ ws, float* __restrict__ x_out, float* __restrict__ u_out,
+                      float* __restrict__ du_sq, float& cost_out, float& alpha_out) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
+  // ---------------- backward: linearise + Riccati + stage costs of the current trajectory
+  {
+    RiccatiState<n, m> rs;
+    rs.init();
+    SweepIn<n, m> cur, nxt;
+    cur.load(C, c, x, u, (size_t)(T - 1) * B + b);
+    for (int t = T - 1; t >= 0; --t) {
+      size_t tb = (size_t)t * B + b;
+      nxt.load(C, c, x, u, (size_t)(t > 0 ? t - 1 : 0) * B + b);      // prefetch step t-1
+      float tau[d], Ctau[d], cb[d];
+#pragma unroll
+      for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) tau[n + a] = cur.u[a];
+      float obj = quad_cost(cur.C, cur.c, tau, Ctau);
+#pragma unroll
+      for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + cur.c[i];
+      float Ft[n][d];
+      if (t < T - 1) {
+        md.jacobian(cur.x, cur.u, Ft);
+      } else {
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int j = 0; j < d; ++j) Ft[i][j] = 0.f;
+      }
+      float zIt[m], lb[m], ub[m];
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        zIt[a] = 0.f; lb[a] = 0.f; ub[a] = 0.f;
+        if constexpr (MODE == GAIN_BOX) {
+          lb[a] = bound_lo(bd, tb * m + a) - cur.u[a];
+          ub[a] = bound_hi(bd, tb * m + a) - cur.u[a];
+        }
+      }
+      float Kt[m][n], kt[m];
+      rs.template step<MODE>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
+      float g[GREC];
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+#pragma unroll
+        for (int j = 0; j < n; ++j) g[a * n + j] = Kt[a][j];
+        g[m * n + a] = kt[a];
+      }
+      g[m * n + m] = obj;
+#pragma unroll
+      for (int i = m * n + m + 1; i < GREC; ++i) g[i] = 0.f;
+      st(ws + tb * GREC, g);
+      cur = nxt;
+    }
+  }
+  // ---------------- forward: line-search rollout (lqr_step_explicit.py:166-263)
+  float alpha = 1.f, cost = 0.f, old_cost = 0.f;
+  for (int ls = 0; ls < max_ls; ++ls) {
+    float xn[n], dx[n];
+    ld(xn, x_init + (size_t)b * n);
+#pragma unroll
+    for (int i = 0; i < n; ++i) dx[i] = 0.f;
+    st(x_out + (size_t)b * n, xn);
+    float cst = 0.f, oldc = 0.f;
+    FwdIn<n, m, GREC> cur, nxt;
+    cur.load(ws, u, C, c, x, (size_t)b, (size_t)(T > 1 ? 1 : 0) * B + b);
+    for (int t = 0; t < T; ++t) {
+      size_t tb = (size_t)t * B + b;
+      {
+        int t1 = t + 1 < T ? t + 1 : t;                 // prefetch step t+1
+        int t2 = t + 2 < T ? t + 2 : t1;
+        nxt.load(ws, u, C, c, x, (size_t)t1 * B + b, (size_t)t2 * B + b);
+      }
+      float nu[m];
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += cur.g[a * n + j] * dx[j];
+        nu[a] = (s + cur.u[a]) + alpha * cur.g[m * n + a];
+        if (bd.mode != DILQR_BOUNDS_NONE) nu[a] = eclamp(nu[a], bound_lo(bd, tb * m + a), bound_hi(bd, tb * m + a));
+      }
+      oldc += cur.g[m * n + m];
+      st(u_out + tb * m, nu);
+      if (ls == 0) {
+#pragma unroll
+        for (int a = 0; a < m; ++a) {
+          float e = cur.u[a] - nu[a];
+          du_sq[((size_t)t * m + a) * B + b] = e * e;
+        }
+      }
+      float tau[d];
+#pragma unroll
+      for (int i = 0; i < n; ++i) tau[i] = xn[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) tau[n + a] = nu[a];
+      cst += quad_cost(cur.C, cur.c, tau);
+      if (t < T - 1) {
+        float xnext[n];
+        md.forward(xn, nu, xnext);
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+          dx[i] = xnext[i] - cur.xnext[i];
+          xn[i] = xnext[i];
+        }
+        st(x_out + (tb + B) * n, xn);
+      }
+      cur = nxt;
+    }
+    cost = cst;
+    if (ls == 0) old_cost = oldc;
+    if (!(cost > old_cost) || ls == max_ls - 1) break;
+    alpha *= decay;
+  }
+  cost_out = cost;
+  alpha_out = alpha;
+}
+
 template <class Model, int MODE>
 __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const float* __restrict__ theta,
                                                          const float* __restrict__ x_init, const float* __restrict__ C,
@@ -383,69 +530,134 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
                                                          float* __restrict__ u_out, float* __restrict__ cost_out,
                                                          float* __restrict__ du_sq, float* __restrict__ alpha_out,
                                                          const dilqr_mpc_ctrl* __restrict__ ctrl) {
-  constexpr int n = Model::N, m = Model::M, d = n + m;
-  constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
   if (ctrl && ctrl->stopped) return;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   Model md; md.load(theta);
-  RiccatiState<n, m> rs;
-  rs.init();
-  for (int t = T - 1; t >= 0; --t) {
-    size_t tb = (size_t)t * B + b;
-    float Ct[d][d], ct[d], xt[n], ut[m];
-    ld2(Ct, C + tb * d * d); ld(ct, c + tb * d); ld(xt, x + tb * n); ld(ut, u + tb * m);
-    float tau[d], Ctau[d], cb[d];
-#pragma unroll
-    for (int i = 0; i < n; ++i) tau[i] = xt[i];
-#pragma unroll
-    for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
-    float obj = quad_cost(Ct, ct, tau, Ctau);
-#pragma unroll
-    for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + ct[i];
-    float Ft[n][d];
-    if (t < T - 1) {
-      md.jacobian(xt, ut, Ft);
-    } else {
-#pragma unroll
-      for (int i = 0; i < n; ++i)
-#pragma unroll
-        for (int j = 0; j < d; ++j) Ft[i][j] = 0.f;
-    }
-    float zIt[m], lb[m], ub[m];
-#pragma unroll
-    for (int a = 0; a < m; ++a) {
-      zIt[a] = 0.f; lb[a] = 0.f; ub[a] = 0.f;
-      if constexpr (MODE == GAIN_BOX) {
-        lb[a] = bound_lo(bd, tb * m + a) - ut[a];
-        ub[a] = bound_hi(bd, tb * m + a) - ut[a];
-      }
-    }
-    float Kt[m][n], kt[m];
-    rs.template step<MODE>(Ct, cb, Ft, zIt, lb, ub, Kt, kt);
-    float g[GREC];
-#pragma unroll
-    for (int a = 0; a < m; ++a) {
-#pragma unroll
-      for (int j = 0; j < n; ++j) g[a * n + j] = Kt[a][j];
-      g[m * n + a] = kt[a];
-    }
-    g[m * n + m] = obj;
-#pragma unroll
-    for (int i = m * n + m + 1; i < GREC; ++i) g[i] = 0.f;
-    st(ws + tb * GREC, g);
-  }
-  Dyn<n, m, Model> dyn;
-  dyn.md = md; dyn.F = nullptr; dyn.f = nullptr; dyn.B = B;
-  float alpha = 1.f, cost = 0.f, old_cost = 0.f;
-  for (int ls = 0; ls < max_ls; ++ls) {
-    cost = forward_pass<n, m, GREC>(dyn, T, B, b, alpha, x_init, C, c, x, u, nullptr, nullptr, ws, bd, nullptr,
-                                    x_out, u_out, ls == 0 ? du_sq : nullptr, ls == 0 ? &old_cost : nullptr);
-    if (!(cost > old_cost) || ls == max_ls - 1) break;
-    alpha *= decay;
-  }
+  float cost, alpha;
+  ilqr_problem<Model, MODE>(T, B, b, md, x_init, C, c, x, u, bd, decay, max_ls, ws, x_out, u_out, du_sq, cost,
+                            alpha);
   cost_out[b] = cost;
   alpha_out[b] = alpha;
+}
+
+// ---------------- the device-resident MPC loop with per-problem trajectory slots
+// Three trajectory buffers per problem ([3,T,B,n] / [3,T,B,m]); each problem
+// keeps the index of its current and best slot, so "best = this iterate"
+// (mpc_explicit.py:277-283) is an index update, never a copy.
+using MpcState = dilqr_mpc_state;
+
+template <class Model, int MODE>
+__global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const float* __restrict__ theta,
+                                                        const float* __restrict__ x_init, const float* __restrict__ C,
+                                                        const float* __restrict__ c, Bounds bd, float decay, int max_ls,
+                                                        int first, float best_cost_eps, MpcState S) {
+  constexpr int n = Model::N, m = Model::M;
+  if (S.ctrl->stopped) return;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Model md; md.load(theta);
+  const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
+  int cur = S.slot[b], best = S.slot[B + b];
+  int nw = (cur != 0 && best != 0) ? 0 : ((cur != 1 && best != 1) ? 1 : 2);
+  float cost, alpha;
+  ilqr_problem<Model, MODE>(T, B, b, md, x_init, C, c, S.X3 + cur * TBn, S.U3 + cur * TBm, bd, decay, max_ls, S.ws,
+                            S.X3 + nw * TBn, S.U3 + nw * TBm, S.du_sq, cost, alpha);
+  S.cost[b] = cost;
+  S.alpha[b] = alpha;
+  bool better = !first && (cost <= S.best_cost[b] + best_cost_eps);      // mpc_explicit.py:278
+  if (first || better) {
+    S.best_cost[b] = cost;
+    S.slot[B + b] = (unsigned char)nw;
+  }
+  S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
+  S.slot[b] = (unsigned char)nw;
+}
+
+// full_du_norm (the reference's batch-mixing rows), best_du for the problems
+// that took this iterate, then — in the last workgroup to finish — the stop
+// rule (mpc_explicit.py:264, 279, 297-299).  Cross-workgroup hand-off: every
+// workgroup's contributions are device-scope atomics; a release fence before and
+// an acquire fence after the arrival counter make them visible to the last one.
+__global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float eps, int not_improved_lim,
+                                                          MpcState S) {
+  __shared__ int last;
+  if (S.ctrl->stopped) return;
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < B) {
+    float s = 0.f;
+    const float* p = S.du_sq + (size_t)r * TM;
+    for (int i = 0; i < TM; ++i) s += p[i];
+    float fdn = sqrtf(s);
+    S.full_du_norm[r] = fdn;
+    atomicMax(&S.ctrl->max_du_bits, __float_as_uint(fdn));
+    int imp = S.improved[r];
+    if (imp) S.best_du[r] = fdn;
+    if (imp == 2) atomicOr(&S.ctrl->any_improved, 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    unsigned prev = atomicAdd(S.done_counter, 1u);
+    last = (prev == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    dilqr_mpc_ctrl* ctl = S.ctrl;
+    int any = __hip_atomic_load(&ctl->any_improved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned mxb = __hip_atomic_load(&ctl->max_du_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ctl->iter += 1;
+    ctl->n_not_improved += 1;
+    if (any) ctl->n_not_improved = 0;
+    if (__uint_as_float(mxb) < eps || ctl->n_not_improved > not_improved_lim) ctl->stopped = 1;
+    __hip_atomic_store(&ctl->any_improved, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctl->max_du_bits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(S.done_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl.
+template <class Model>
+__global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float* __restrict__ theta,
+                                                      const float* __restrict__ x_init, MpcState S) {
+  constexpr int n = Model::N, m = Model::M;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b == 0) {
+    dilqr_mpc_ctrl z = {};
+    *S.ctrl = z;
+    *S.done_counter = 0u;
+  }
+  if (b >= B) return;
+  Model md; md.load(theta);
+  S.slot[b] = 0; S.slot[B + b] = 0;
+  float xt[n];
+  ld(xt, x_init + (size_t)b * n);
+  st(S.X3 + (size_t)b * n, xt);
+  for (int t = 0; t < T - 1; ++t) {
+    float ut[m], xn[n];
+    ld(ut, S.U3 + ((size_t)t * B + b) * m);
+    md.forward(xt, ut, xn);
+#pragma unroll
+    for (int i = 0; i < n; ++i) xt[i] = xn[i];
+    st(S.X3 + ((size_t)(t + 1) * B + b) * n, xt);
+  }
+}
+
+template <int n, int m>
+__global__ void __launch_bounds__(kBlock) k_mpc_gather(int T, int B, MpcState S, float* __restrict__ x_out,
+                                                       float* __restrict__ u_out) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int best = S.slot[B + b];
+  const float* X = S.X3 + (size_t)best * T * B * n;
+  const float* U = S.U3 + (size_t)best * T * B * m;
+  for (int t = 0; t < T; ++t) {
+    size_t tb = (size_t)t * B + b;
+    float xt[n], ut[m];
+    ld(xt, X + tb * n); ld(ut, U + tb * m);
+    st(x_out + tb * n, xt); st(u_out + tb * m, ut);
+  }
 }
 
 // ============================================================ MPC bookkeeping
@@ -1250,6 +1462,58 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta, con
   MODEL_SWITCH(model, (k_implicit_backward<MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
                           T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta)));
   return launched();
+}
+
+
+static bool bad_state(const dilqr_mpc_state& st) {
+  return !st.X3 || !st.U3 || !st.slot || !st.best_cost || !st.best_du || !st.improved || !st.cost || !st.alpha ||
+         !st.du_sq || !st.full_du_norm || !st.ws || !st.ctrl || !st.done_counter || !al16(st.X3) || !al16(st.U3) ||
+         !al16(st.ws);
+}
+
+int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init, dilqr_mpc_state st,
+                        void* stream) {
+  if (T < 1 || B < 0 || !theta || !x_init || !al16(x_init) || bad_state(st)) return DILQR_E_ARG;
+  MODEL_SWITCH(model, (k_mpc_begin<MD><<<grid_for(B > 0 ? B : 1), kBlock, 0, S(stream)>>>(T, B, theta, x_init, st)));
+  return launched();
+}
+
+int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
+                          const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
+                          int first, float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st,
+                          void* stream) {
+  if (T < 1 || B < 0 || max_linesearch_iter < 1 || !theta || !x_init || !C || !c) return DILQR_E_ARG;
+  if (!al16(x_init) || !al16(C) || !al16(c) || bad_state(st) || bad_bounds(bounds)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  Bounds bd = mkb(bounds);
+  bool box = bounds.mode != DILQR_BOUNDS_NONE;
+  int m_ = 0;
+  MODEL_SWITCH(model, ({
+    m_ = MD::M;
+    if (box)
+      k_mpc_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, bd,
+                                                                        linesearch_decay, max_linesearch_iter,
+                                                                        first, best_cost_eps, st);
+    else
+      k_mpc_iterate<MD, GAIN_UNC><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, bd,
+                                                                        linesearch_decay, max_linesearch_iter,
+                                                                        first, best_cost_eps, st);
+  }));
+  int e = launched();
+  if (e) return e;
+  k_mpc_norm_control<<<(B + 255) / 256, 256, 0, S(stream)>>>(T * m_, B, eps, not_improved_lim, st);
+  return launched();
+}
+
+int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out, float* u_out,
+                              void* stream) {
+  if (T < 1 || B < 0 || !x_out || !u_out || !al16(x_out) || !al16(u_out) || bad_state(st)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+#define X(N_, M_) \
+  if (n == N_ && m == M_) { k_mpc_gather<N_, M_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, st, x_out, u_out); return launched(); }
+  DILQR_FOR_EACH_SHAPE(X)
+#undef X
+  return DILQR_E_SHAPE;
 }
 
 }  // extern "C"

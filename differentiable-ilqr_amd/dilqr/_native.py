@@ -27,6 +27,13 @@ class Bounds(ctypes.Structure):
 
 CTRL_INTS = 8          # sizeof(dilqr_mpc_ctrl) / 4
 
+
+class MpcState(ctypes.Structure):
+    """dilqr_mpc_state: device pointers of one MPC solve (include/dilqr.h)."""
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("X3", "U3", "slot", "best_cost", "best_du", "improved", "cost", "alpha", "du_sq",
+                 "full_du_norm", "ws", "ctrl", "done_counter")]
+
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 SIGNATURES = {
     "dilqr_version": ([], _i),
@@ -47,6 +54,9 @@ SIGNATURES = {
     "dilqr_lqr_adjoint_f32": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _i, _vp, _vp, _vp,
                                _vp, _vp, _vp, _vp], _i),
     "dilqr_implicit_ws_floats": ([_i], _i),
+    "dilqr_mpc_begin_f32": ([_i, _i, _i, _vp, _vp, MpcState, _vp], _i),
+    "dilqr_mpc_iterate_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
+    "dilqr_mpc_gather_best_f32": ([_i, _i, _i, _i, MpcState, _vp, _vp, _vp], _i),
     "dilqr_implicit_backward_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _vp, _vp, _vp,
                                      _vp, _vp], _i),
 }

@@ -95,15 +95,12 @@ class MPC(Module):
         theta = ops.theta_of(dx, x_init)
         Cd, cd = C.detach().contiguous(), c.detach().contiguous()
         with torch.no_grad():
-            ws = ops.mpc_solve(model_id, theta, x_init.detach(), Cd, cd, T, u_init=self.u_init,
-                               u_lower=self.u_lower, u_upper=self.u_upper, lqr_iter=self.lqr_iter, eps=self.eps,
-                               linesearch_decay=self.linesearch_decay,
-                               max_linesearch_iter=self.max_linesearch_iter,
-                               not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps)
-        x, u = ws.best_x, ws.best_u
-        costs = ws.best_cost
-        full_du_norm = ws.best_du
-        self.last_iterations = ws.ctrl
+            x, u, costs, full_du_norm, sv = ops.mpc_solve(
+                model_id, theta, x_init.detach(), Cd, cd, T, u_init=self.u_init, u_lower=self.u_lower,
+                u_upper=self.u_upper, lqr_iter=self.lqr_iter, eps=self.eps,
+                linesearch_decay=self.linesearch_decay, max_linesearch_iter=self.max_linesearch_iter,
+                not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps)
+        self.last_solve = sv
 
         need_grad = torch.is_grad_enabled() and self.backprop and (
             C.requires_grad or c.requires_grad or

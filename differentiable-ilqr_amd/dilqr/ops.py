@@ -125,53 +125,85 @@ class MPCWorkspace:
         self.ctrl = torch.zeros(N.CTRL_INTS, dtype=torch.int32, device=dev)
 
 
-def ilqr_iterate(model_id, theta, x_init, C, c, ws, bounds, decay, max_ls, first, best_cost_eps, eps,
-                 not_improved_lim):
-    """One MPC iteration (mpc_explicit.py:246-299) on device: fused iterate kernel
-    (current (xa,ua) -> new (xb,ub)) + best/stop bookkeeping, then swap."""
-    T, B, n = ws.xa.shape
-    m = ws.ua.shape[2]
-    s = N.stream(x_init.device)
-    N.call("dilqr_ilqr_iterate_f32", model_id, T, B, N.ptr(theta), N.ptr(x_init), N.ptr(C), N.ptr(c),
-           N.ptr(ws.xa), N.ptr(ws.ua), bounds, float(decay), int(max_ls), N.ptr(ws.ws), N.ptr(ws.xb),
-           N.ptr(ws.ub), N.ptr(ws.cost), N.ptr(ws.du_sq), N.ptr(ws.alpha), N.ptr(ws.ctrl), s)
-    N.call("dilqr_mpc_update_best_f32", n, m, T, B, int(first), float(best_cost_eps), float(eps),
-           int(min(not_improved_lim, 2 ** 31 - 1)), N.ptr(ws.xb), N.ptr(ws.ub), N.ptr(ws.cost), N.ptr(ws.du_sq),
-           N.ptr(ws.fdn), N.ptr(ws.best_x), N.ptr(ws.best_u), N.ptr(ws.best_cost), N.ptr(ws.best_du),
-           N.ptr(ws.ctrl), s)
-    ws.xa, ws.xb = ws.xb, ws.xa
-    ws.ua, ws.ub = ws.ub, ws.ua
+class MPCSolve:
+    """Device state of one fused MPC solve (dilqr_mpc_state): three trajectory
+    slots per problem, per-problem best bookkeeping, the loop control block."""
+
+    def __init__(self, T, B, n, m, device):
+        dev = device
+        self.T, self.B, self.n, self.m = T, B, n, m
+        self.X3 = torch.empty(3, T, B, n, device=dev)
+        self.U3 = torch.zeros(3, T, B, m, device=dev)
+        self.slot = torch.zeros(2, B, dtype=torch.uint8, device=dev)
+        self.best_cost = torch.empty(B, device=dev)
+        self.best_du = torch.empty(B, device=dev)
+        self.improved = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.cost = torch.empty(B, device=dev)
+        self.alpha = torch.empty(B, device=dev)
+        self.du_sq = torch.empty(T, m, B, device=dev)
+        self.full_du_norm = torch.empty(B, device=dev)
+        self.ws = torch.empty(T * B * grec_floats(n, m), device=dev)
+        self.ctrl = torch.zeros(N.CTRL_INTS, dtype=torch.int32, device=dev)
+        self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.state = N.MpcState(*[t.data_ptr() for t in (
+            self.X3, self.U3, self.slot, self.best_cost, self.best_du, self.improved, self.cost, self.alpha,
+            self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter)])
+
+    def begin(self, model_id, theta, x_init, u_init=None):
+        """x = get_traj(u_init or 0) into slot 0; reset slots and the control block."""
+        if u_init is None:
+            self.U3[0].zero_()
+        else:
+            u0 = u_init.to(device=self.U3.device, dtype=torch.float32)
+            if u0.ndimension() == 2:
+                u0 = u0.unsqueeze(1).expand(self.T, self.B, self.m)
+            self.U3[0].copy_(u0)
+        N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), self.state,
+               N.stream(x_init.device))
+
+    def iterate(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, first, best_cost_eps, eps,
+                not_improved_lim):
+        N.call("dilqr_mpc_iterate_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), N.ptr(C),
+               N.ptr(c), bounds, float(decay), int(max_ls), int(first), float(best_cost_eps), float(eps),
+               int(min(not_improved_lim, 2 ** 31 - 1)), self.state, N.stream(x_init.device))
+
+    def gather_best(self):
+        x = torch.empty(self.T, self.B, self.n, device=self.X3.device)
+        u = torch.empty(self.T, self.B, self.m, device=self.X3.device)
+        N.call("dilqr_mpc_gather_best_f32", self.n, self.m, self.T, self.B, self.state, N.ptr(x), N.ptr(u),
+               N.stream(x.device))
+        return x, u
+
+    @property
+    def stopped(self):
+        return bool(int(self.ctrl[1].item()))
+
+    @property
+    def iterations(self):
+        return int(self.ctrl[0].item())
 
 
 def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upper=None, lqr_iter=10,
               eps=1e-7, linesearch_decay=0.2, max_linesearch_iter=10, not_improved_lim=5, best_cost_eps=1e-4,
               check_every=8):
     """The iLQR outer loop of mpc_explicit.MPC.forward (mpc_explicit.py:228-299)
-    entirely on device; the host only reads the stop flag every `check_every`
-    iterations.  Returns the workspace (best_x, best_u, best_cost, best_du, ctrl)."""
+    entirely on device (fused iterate kernel + norm/stop kernel per iteration);
+    the host only polls the stop flag every `check_every` iterations.
+    Returns (best_x, best_u, best_cost, best_du, solve)."""
     B, n = x_init.shape
     m = C.shape[-1] - n
-    dev = x_init.device
     x_init, C, c = _f32(x_init), _f32(C), _f32(c)
-    ws = MPCWorkspace(T, B, n, m, dev)
-    if u_init is None:
-        ws.ua.zero_()
-    else:
-        u0 = u_init.to(device=dev, dtype=torch.float32)
-        if u0.ndimension() == 2:
-            u0 = u0.unsqueeze(1).expand(T, B, m)
-        ws.ua.copy_(u0)
+    sv = MPCSolve(T, B, n, m, x_init.device)
+    sv.begin(model_id, theta, x_init, u_init)
     bounds, keep = N.make_bounds(u_lower, u_upper)
-    N.call("dilqr_rollout_f32", model_id, n, m, T, B, N.ptr(theta), None, None, N.ptr(x_init), N.ptr(ws.ua),
-           N.ptr(ws.xa), N.stream(dev))
     for i in range(lqr_iter):
-        ilqr_iterate(model_id, theta, x_init, C, c, ws, bounds, linesearch_decay, max_linesearch_iter, i == 0,
-                     best_cost_eps, eps, not_improved_lim)
-        if check_every and (i + 1) % check_every == 0 and i + 1 < lqr_iter:
-            if int(ws.ctrl[1].item()):
-                break
+        sv.iterate(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i == 0,
+                   best_cost_eps, eps, not_improved_lim)
+        if check_every and (i + 1) % check_every == 0 and i + 1 < lqr_iter and sv.stopped:
+            break
     del keep
-    return ws
+    x, u = sv.gather_best()
+    return x, u, sv.best_cost, sv.best_du, sv
 
 
 def lqr_adjoint(C, c, F, x, u, dl_dx, dl_du, u_lower=None, u_upper=None, m_solver=N.SOLVE_INV, want_df=True):

@@ -188,6 +188,38 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
                                 const float* dl_du, dilqr_bounds bounds, float* ws,
                                 float* dC, float* dc, float* dtheta, void* stream);
 
+/* ---- the device-resident MPC loop with per-problem trajectory slots ------ */
+/* Caller-owned device buffers of one solve.  X3 [3,T,B,n] and U3 [3,T,B,m] hold
+   three trajectories per problem; slot [2,B] (uint8) the indices of each
+   problem's current and best one, so taking an iterate as the new best
+   (mpc_explicit.py:277-283) moves no data.  ws: T*B*ceil4(m*n+m+1) floats.
+   done_counter: one uint (zeroed by begin). */
+typedef struct dilqr_mpc_state {
+  float* X3; float* U3; unsigned char* slot; float* best_cost; float* best_du;
+  int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;
+  float* ws; dilqr_mpc_ctrl* ctrl; unsigned* done_counter;
+} dilqr_mpc_state;
+
+/* Start a solve: x = get_traj(u) from the controls the caller placed in U3
+   slot 0 (zeros or u_init), slots/ctrl reset (mpc_explicit.py:228-249). */
+int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init,
+                        dilqr_mpc_state st, void* stream);
+
+/* One MPC iteration (mpc_explicit.py:246-299): the fused linearise + Riccati
+   (+pnqp) + line-search kernel on each problem's current slot, best-iterate
+   slot update, then the quirk full_du_norm, best_du and the batch-global stop
+   rule (max du < eps or n_not_improved > lim) on device.  No-op once stopped.
+   first != 0 for iteration 0. */
+int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const float* x_init,
+                          const float* C, const float* c, dilqr_bounds bounds,
+                          float linesearch_decay, int max_linesearch_iter, int first,
+                          float best_cost_eps, float eps, int not_improved_lim,
+                          dilqr_mpc_state st, void* stream);
+
+/* Materialise each problem's best trajectory into x_out [T,B,n], u_out [T,B,m]. */
+int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out,
+                              float* u_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
