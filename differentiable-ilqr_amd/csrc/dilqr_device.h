@@ -296,6 +296,12 @@ DEV int pnqp(const float (&H)[M][M], const float (&q)[M], const float (&lb)[M],
 //   out: K_t [M][N], k_t [M]; V/v of step t.
 enum GainMode { GAIN_UNC = 0, GAIN_CHOL = 1, GAIN_ZERO_I = 2, GAIN_BOX = 3 };
 
+// Dense F by default; a model's Jacobian can declare its structural zeros
+// (static constexpr bool nz(i, j)) so the fused kernel skips those products.
+struct DenseF {
+  static constexpr bool nz(int, int) { return true; }
+};
+
 template <int N, int M>
 struct RiccatiState {
   static constexpr int D = N + M;
@@ -320,7 +326,7 @@ struct RiccatiState {
 
   // mode GAIN_ZERO_I uses zI[M] (1 = active); GAIN_BOX uses lb/ub [M] (already
   // lower-u_t / upper-u_t, lqr_step_explicit.py:132-133).
-  template <int MODE>
+  template <int MODE, class FS = DenseF>
   DEV void step(const float (&C)[D][D], const float (&cb)[D], const float (&F)[N][D],
                 const float (&zI)[M], const float (&lb)[M], const float (&ub)[M],
                 float (&K)[M][N], float (&k)[M]) {
@@ -332,7 +338,8 @@ struct RiccatiState {
       for (int kk = 0; kk < N; ++kk) {
         float s = 0.f;
 #pragma unroll
-        for (int l = 0; l < N; ++l) s += F[l][i] * V[l][kk];
+        for (int l = 0; l < N; ++l)
+          if (FS::nz(l, i)) s += F[l][i] * V[l][kk];
         P[i][kk] = s;
       }
     float Q[D][D], q[D];
@@ -342,12 +349,14 @@ struct RiccatiState {
       for (int j = 0; j < D; ++j) {
         float s = 0.f;
 #pragma unroll
-        for (int kk = 0; kk < N; ++kk) s += P[i][kk] * F[kk][j];
+        for (int kk = 0; kk < N; ++kk)
+          if (FS::nz(kk, j)) s += P[i][kk] * F[kk][j];
         Q[i][j] = C[i][j] + s;
       }
       float s = 0.f;
 #pragma unroll
-      for (int l = 0; l < N; ++l) s += F[l][i] * v[l];
+      for (int l = 0; l < N; ++l)
+        if (FS::nz(l, i)) s += F[l][i] * v[l];
       q[i] = cb[i] + s;
     }
     // partitions (lqr_step_explicit.py:78-83)
@@ -476,19 +485,11 @@ struct RiccatiState {
 };
 
 // 0.5*bquad(tau, C) + bdot(tau, c)  (util.py:130-153 / lqr_step_explicit.py:234);
-// also returns C tau (for c_back = C tau + c).
+// also returns C tau (for c_back = C tau + c), and forms the quadratic term as
+// tau . (C tau) so the product is computed once.
 template <int D>
 DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D],
                     float (&Ctau)[D]) {
-  // bquad = (tau^T C) tau
-  float quad = 0.f;
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    float r = 0.f;
-#pragma unroll
-    for (int i = 0; i < D; ++i) r += tau[i] * C[i][j];
-    quad += r * tau[j];
-  }
 #pragma unroll
   for (int i = 0; i < D; ++i) {
     float s = 0.f;
@@ -496,9 +497,12 @@ DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&t
     for (int j = 0; j < D; ++j) s += C[i][j] * tau[j];
     Ctau[i] = s;
   }
-  float lin = 0.f;
+  float quad = 0.f, lin = 0.f;
 #pragma unroll
-  for (int i = 0; i < D; ++i) lin += tau[i] * c[i];
+  for (int i = 0; i < D; ++i) {
+    quad += tau[i] * Ctau[i];
+    lin += tau[i] * c[i];
+  }
   return 0.5f * quad + lin;
 }
 

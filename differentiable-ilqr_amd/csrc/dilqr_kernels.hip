@@ -145,38 +145,50 @@ __global__ void __launch_bounds__(kBlock) k_lqr_backward(int T, int B, const flo
   if (b >= B) return;
   RiccatiState<n, m> rs;
   rs.init();
+  // per-step inputs, software-pipelined one step ahead (see ilqr_problem)
+  struct In {
+    float C[d][d], c[d], F[n][d], x[n], u[m];
+    DEV void load(const float* Cp, const float* cp, const float* Fp, const float* xp, const float* up, int t, int T,
+                  int B, int b) {
+      size_t tb = (size_t)t * B + b;
+      ld2(C, Cp + tb * d * d);
+      ld(c, cp + tb * d);
+      size_t tf = (size_t)(t < T - 1 ? t : (T > 1 ? T - 2 : 0)) * B + b;   // F[T-1] does not exist
+      if (T > 1) ld2(F, Fp + tf * n * d);
+      if (xp) ld(x, xp + tb * n);
+      if (up) ld(u, up + tb * m);
+    }
+  } cur, nxt;
+#pragma unroll
+  for (int i = 0; i < n; ++i) cur.x[i] = nxt.x[i] = 0.f;
+#pragma unroll
+  for (int a = 0; a < m; ++a) cur.u[a] = nxt.u[a] = 0.f;
+  cur.load(C, c, F, x, u, T - 1, T, B, b);
   for (int t = T - 1; t >= 0; --t) {
     size_t tb = (size_t)t * B + b;
-    float Ct[d][d], cb[d];
-    ld2(Ct, C + tb * d * d);
-    ld(cb, c + tb * d);
-    float ut[m];
+    nxt.load(C, c, F, x, u, t > 0 ? t - 1 : 0, T, B, b);
+    float cb[d];
 #pragma unroll
-    for (int a = 0; a < m; ++a) ut[a] = 0.f;
-    if (u) ld(ut, u + tb * m);
+    for (int i = 0; i < d; ++i) cb[i] = cur.c[i];
     if (x) {
-      float tau[d], xt[n];
-      ld(xt, x + tb * n);
+      float tau[d];
 #pragma unroll
-      for (int i = 0; i < n; ++i) tau[i] = xt[i];
+      for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
 #pragma unroll
-      for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+      for (int a = 0; a < m; ++a) tau[n + a] = cur.u[a];
 #pragma unroll
       for (int i = 0; i < d; ++i) {
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < d; ++j) s += Ct[i][j] * tau[j];
+        for (int j = 0; j < d; ++j) s += cur.C[i][j] * tau[j];
         cb[i] = s + cb[i];
       }
     }
-    float Ft[n][d];
-    if (t < T - 1) {
-      ld2(Ft, F + tb * n * d);
-    } else {
+    if (t == T - 1) {
 #pragma unroll
       for (int i = 0; i < n; ++i)
 #pragma unroll
-        for (int j = 0; j < d; ++j) Ft[i][j] = 0.f;
+        for (int j = 0; j < d; ++j) cur.F[i][j] = 0.f;
     }
     float zIt[m], lb[m], ub[m];
 #pragma unroll
@@ -184,14 +196,15 @@ __global__ void __launch_bounds__(kBlock) k_lqr_backward(int T, int B, const flo
       zIt[a] = 0.f; lb[a] = 0.f; ub[a] = 0.f;
       if constexpr (MODE == GAIN_ZERO_I) zIt[a] = zI[tb * m + a] ? 1.f : 0.f;
       if constexpr (MODE == GAIN_BOX) {
-        lb[a] = bound_lo(bd, tb * m + a) - ut[a];
-        ub[a] = bound_hi(bd, tb * m + a) - ut[a];
+        lb[a] = bound_lo(bd, tb * m + a) - cur.u[a];
+        ub[a] = bound_hi(bd, tb * m + a) - cur.u[a];
       }
     }
     float Kt[m][n], kt[m];
-    rs.template step<MODE>(Ct, cb, Ft, zIt, lb, ub, Kt, kt);
+    rs.template step<MODE>(cur.C, cb, cur.F, zIt, lb, ub, Kt, kt);
     st2(K + tb * m * n, Kt);
     st(k + tb * m, kt);
+    cur = nxt;
   }
   if (n_qp) n_qp[b] = rs.n_qp;
 }
@@ -443,7 +456,7 @@ DEV void ilqr_problem(int T, int B, int b, const Model& md, const float* __restr
         }
       }
       float Kt[m][n], kt[m];
-      rs.template step<MODE>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
+      rs.template step<MODE, typename Model::FSparsity>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
       float g[GREC];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
@@ -581,22 +594,40 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
 // an acquire fence after the arrival counter make them visible to the last one.
 __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float eps, int not_improved_lim,
                                                           MpcState S) {
+  __shared__ unsigned red_max[4];
+  __shared__ int red_any[4];
   __shared__ int last;
   if (S.ctrl->stopped) return;
   int r = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned mx = 0u;
+  int any = 0;
   if (r < B) {
     float s = 0.f;
     const float* p = S.du_sq + (size_t)r * TM;
     for (int i = 0; i < TM; ++i) s += p[i];
     float fdn = sqrtf(s);
     S.full_du_norm[r] = fdn;
-    atomicMax(&S.ctrl->max_du_bits, __float_as_uint(fdn));
+    mx = __float_as_uint(fdn);              // fdn >= 0: float order == uint order
     int imp = S.improved[r];
     if (imp) S.best_du[r] = fdn;
-    if (imp == 2) atomicOr(&S.ctrl->any_improved, 1);
+    any = imp == 2;
   }
+  // wave reduction (64 lanes), then across the block's 4 waves, one atomic per block
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    unsigned o = __shfl_xor(mx, off, 64);
+    mx = o > mx ? o : mx;
+    any |= __shfl_xor(any, off, 64);
+  }
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red_max[w] = mx; red_any[w] = any; }
   __syncthreads();
   if (threadIdx.x == 0) {
+    unsigned bm = red_max[0];
+    int ba = red_any[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { bm = red_max[i] > bm ? red_max[i] : bm; ba |= red_any[i]; }
+    atomicMax(&S.ctrl->max_du_bits, bm);
+    if (ba) atomicOr(&S.ctrl->any_improved, 1);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     unsigned prev = atomicAdd(S.done_counter, 1u);
     last = (prev == gridDim.x - 1);
@@ -605,11 +636,11 @@ __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float e
   if (last && threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     dilqr_mpc_ctrl* ctl = S.ctrl;
-    int any = __hip_atomic_load(&ctl->any_improved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int anyi = __hip_atomic_load(&ctl->any_improved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned mxb = __hip_atomic_load(&ctl->max_du_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ctl->iter += 1;
     ctl->n_not_improved += 1;
-    if (any) ctl->n_not_improved = 0;
+    if (anyi) ctl->n_not_improved = 0;
     if (__uint_as_float(mxb) < eps || ctl->n_not_improved > not_improved_lim) ctl->stopped = 1;
     __hip_atomic_store(&ctl->any_improved, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&ctl->max_du_bits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

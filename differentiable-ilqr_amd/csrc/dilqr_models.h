@@ -17,6 +17,10 @@ struct Pendulum {
   float g, m, l;
   DEV void load(const float* __restrict__ th) { g = th[0]; m = th[1]; l = th[2]; }
 
+  struct FSparsity {      // pendulum.py:448-474: row 2 has a structural zero at cos
+    static constexpr bool nz(int i, int j) { return !(i == 2 && j == 0); }
+  };
+
   // pendulum.py:60-95
   DEV void forward(const float (&x)[N], const float (&u)[M], float (&o)[N]) const {
 #pragma clang fp contract(off)
@@ -59,6 +63,13 @@ struct Cartpole {
   float g, mc, mp, l;
   DEV void load(const float* __restrict__ th) { g = th[0]; mc = th[1]; mp = th[2]; l = th[3]; }
 
+  // structural nonzeros of jacobian() (cartpole.py:802-838): rows x, dx, cos, sin, dth
+  struct FSparsity {
+    static constexpr bool nz(int i, int j) {
+      return i == 0 ? (j <= 1) : i == 1 ? (j >= 1) : i == 4 ? (j >= 2) : (j >= 2 && j <= 4);
+    }
+  };
+
   // cartpole.py:64-97
   DEV void forward(const float (&s_)[N], const float (&u)[M], float (&o)[N]) const {
 #pragma clang fp contract(off)
@@ -99,13 +110,13 @@ struct Cartpole {
     float xa_s = A_s * iM - k * tha_s * c;
     float xa_w = A_w * iM - k * tha_w * c;
     float xa_u = iM - k * tha_u * c;
-    float r2 = c * c + s * s;
+    float ir2 = 1.0f / (c * c + s * s);
     float th2 = DT * w + atan2f(s, c);
     float sn = sinf(th2), cs = cosf(th2);
     D[0][0] = 1.f; D[0][1] = DT;  D[0][2] = 0.f;            D[0][3] = 0.f;            D[0][4] = 0.f;            D[0][5] = 0.f;
     D[1][0] = 0.f; D[1][1] = 1.f; D[1][2] = DT * xa_c;      D[1][3] = DT * xa_s;      D[1][4] = DT * xa_w;      D[1][5] = DT * xa_u;
-    D[2][0] = 0.f; D[2][1] = 0.f; D[2][2] = s * sn / r2;    D[2][3] = -c * sn / r2;   D[2][4] = -DT * sn;       D[2][5] = 0.f;
-    D[3][0] = 0.f; D[3][1] = 0.f; D[3][2] = -s * cs / r2;   D[3][3] = c * cs / r2;    D[3][4] = DT * cs;        D[3][5] = 0.f;
+    D[2][0] = 0.f; D[2][1] = 0.f; D[2][2] = s * sn * ir2;   D[2][3] = -c * sn * ir2;  D[2][4] = -DT * sn;       D[2][5] = 0.f;
+    D[3][0] = 0.f; D[3][1] = 0.f; D[3][2] = -s * cs * ir2;  D[3][3] = c * cs * ir2;   D[3][4] = DT * cs;        D[3][5] = 0.f;
     D[4][0] = 0.f; D[4][1] = 0.f; D[4][2] = DT * tha_c;     D[4][3] = DT * tha_s;     D[4][4] = 1.f + DT * tha_w; D[4][5] = DT * tha_u;
   }
 };
