@@ -191,6 +191,7 @@ def main():
     if os.path.exists(pmc_path):
         try:
             traffic = json.load(open(pmc_path)).get("k_ilqr_iterate_bytes_per_launch")
+            traffic = None if traffic is None else traffic * B / B_PER_GPU
         except Exception:
             traffic = None
 

@@ -1,0 +1,559 @@
+// dilqr_group.h — 16 lanes per problem for the larger models (d = n+m <= 16,
+// rocket: n=13 m=3).  Included by dilqr_kernels.hip.
+//
+// One lane per problem stops fitting once a step's matrices (C 16x16, F 13x16,
+// V 13x13) exceed the register file, so here a problem is a 16-lane group of a
+// wave (4 problems per wave, one wave per workgroup) and lane r owns ROW r:
+// C row r streams from HBM (64 contiguous bytes per lane, 1 KiB per problem),
+// V, v, F and the u-rows of Q are exchanged through the workgroup's LDS, and
+// the m x m gain solve (and pnqp) runs redundantly in every lane of the group,
+// so every lane holds K and k in registers.  Cross-lane sums use 16-lane xor
+// shuffles.  Same math as RiccatiState::step (lqr_step_explicit.py:63-160).
+#pragma once
+#include <type_traits>
+
+#include "dilqr_device.h"
+
+namespace dilqr {
+
+constexpr int kG = 16;          // lanes per problem
+constexpr int kGPW = 64 / kG;   // problems per wave (= per workgroup)
+
+struct GroupNoModel {           // LinDx dynamics (F, f given)
+  DEV void load(const float*) {}
+};
+
+DEV float group_sum(float v) {
+#pragma unroll
+  for (int off = kG / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kG);
+  return v;
+}
+
+template <int n, int m>
+struct GroupLds {
+  static constexpr int d = n + m;
+  static constexpr int W = 16;                 // padded row width (b128 reads)
+  float V[n][W];
+  float v[W];
+  float F[n][W];
+  float Qu[m][W + 4];                          // u rows of Q, q_u at [.][W]
+  float Kk[m][W + 4];                          // gains K, k at [.][W]
+  float tau[W];
+};
+
+// gains from the u-rows of Q, identical in every lane (modes as RiccatiState)
+template <int n, int m, int MODE>
+DEV void group_gains(const float (&Quu)[m][m], const float (&Qux)[m][n], const float (&qu)[m],
+                     const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&K)[m][n],
+                     float (&k)[m], float (&prev_k)[m], bool& have_prev, int& n_qp) {
+  if constexpr (MODE == GAIN_UNC || MODE == GAIN_CHOL) {
+    float A[m][m], X[m][n + 1];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+#pragma unroll
+      for (int b = 0; b < m; ++b) A[a][b] = Quu[a][b] + ((MODE == GAIN_CHOL && a == b) ? 1e-6f : 0.f);
+#pragma unroll
+      for (int j = 0; j < n; ++j) X[a][j] = Qux[a][j];
+      X[a][n] = qu[a];
+    }
+    if constexpr (MODE == GAIN_CHOL) chol_solve<m, n + 1>(A, X);
+    else gauss_solve<m, n + 1>(A, X);
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+#pragma unroll
+      for (int j = 0; j < n; ++j) K[a][j] = -X[a][j];
+      k[a] = -X[a][n];
+    }
+  } else if constexpr (MODE == GAIN_ZERO_I) {
+    float A[m][m], X[m][n + 1];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      bool Ia = zI[a] != 0.f;
+#pragma unroll
+      for (int b = 0; b < m; ++b) {
+        bool fr = (zI[a] == 0.f) && (zI[b] == 0.f);
+        A[a][b] = (fr ? Quu[a][b] : 0.f) + ((a == b && Ia) ? 1e-8f : 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < n; ++j) X[a][j] = Ia ? 0.f : Qux[a][j];
+      X[a][n] = Ia ? 0.f : qu[a];
+    }
+    gauss_solve<m, n + 1>(A, X);
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+#pragma unroll
+      for (int j = 0; j < n; ++j) K[a][j] = -X[a][j];
+      k[a] = -X[a][n];
+    }
+  } else {                                        // GAIN_BOX: pnqp
+    float x[m], If[m], Hf[m][m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) x[a] = prev_k[a];
+    int it = pnqp<m>(Quu, qu, lb, ub, have_prev, x, If, Hf);
+    n_qp += 1 + it;
+#pragma unroll
+    for (int a = 0; a < m; ++a) { k[a] = x[a]; prev_k[a] = x[a]; }
+    have_prev = true;
+    float X[m][n];
+#pragma unroll
+    for (int a = 0; a < m; ++a)
+#pragma unroll
+      for (int j = 0; j < n; ++j) X[a][j] = If[a] != 0.f ? Qux[a][j] : 0.f;
+    gauss_solve<m, n>(Hf, X);
+#pragma unroll
+    for (int a = 0; a < m; ++a)
+#pragma unroll
+      for (int j = 0; j < n; ++j) K[a][j] = -X[a][j];
+  }
+}
+
+// One backward Riccati step for the group's problem; lane r owns rows r of
+// C/Q/P/V.  Crow: C_t row r, cb_r: c_back_t[r] (both only meaningful for r < d).
+// F_t rows are already in L.F (zero for t = T-1), V/v of step t+1 in L.V / L.v.
+// On return the gains are in K/k (all lanes) and L.Kk, V/v of step t in L.
+template <int n, int m, int MODE>
+DEV void group_riccati_step(GroupLds<n, m>& L, int r, const float (&Crow)[n + m], float cb_r,
+                            const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&K)[m][n],
+                            float (&k)[m], float (&prev_k)[m], bool& have_prev, int& n_qp) {
+  constexpr int d = n + m;
+  const bool row = r < d;
+  // P row r = F[:, r]^T V ; q_r = cb_r + F[:, r] . v
+  float Fcol[n], P[n];
+#pragma unroll
+  for (int l = 0; l < n; ++l) Fcol[l] = row ? L.F[l][r] : 0.f;
+#pragma unroll
+  for (int kk = 0; kk < n; ++kk) P[kk] = 0.f;
+#pragma unroll
+  for (int l = 0; l < n; ++l) {
+#pragma unroll
+    for (int kk = 0; kk < n; ++kk) P[kk] += Fcol[l] * L.V[l][kk];
+  }
+  float qr = 0.f;
+#pragma unroll
+  for (int l = 0; l < n; ++l) qr += Fcol[l] * L.v[l];
+  qr = cb_r + qr;
+  // Q row r = C row r + P row r F
+  float Q[d];
+#pragma unroll
+  for (int j = 0; j < d; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < n; ++kk) s += P[kk] * L.F[kk][j];
+    Q[j] = Crow[j] + s;
+  }
+  if (r >= n && r < d) {
+#pragma unroll
+    for (int j = 0; j < d; ++j) L.Qu[r - n][j] = Q[j];
+    L.Qu[r - n][GroupLds<n, m>::W] = qr;
+  }
+  __syncthreads();
+  float Quu[m][m], Qux[m][n], qu[m];
+#pragma unroll
+  for (int a = 0; a < m; ++a) {
+#pragma unroll
+    for (int b = 0; b < m; ++b) Quu[a][b] = L.Qu[a][n + b];
+#pragma unroll
+    for (int j = 0; j < n; ++j) Qux[a][j] = L.Qu[a][j];
+    qu[a] = L.Qu[a][GroupLds<n, m>::W];
+  }
+  group_gains<n, m, MODE>(Quu, Qux, qu, zI, lb, ub, K, k, prev_k, have_prev, n_qp);
+  // K[a][r] (this lane's column) from registers without a runtime index: the
+  // group leader publishes K, k in LDS
+  if ((r & (kG - 1)) == 0) {
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+#pragma unroll
+      for (int j = 0; j < n; ++j) L.Kk[a][j] = K[a][j];
+      L.Kk[a][GroupLds<n, m>::W] = k[a];
+    }
+  }
+  __syncthreads();
+  if (r < n) {
+    float Kc[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) Kc[a] = L.Kk[a][r];
+    float KcQuu[m];
+#pragma unroll
+    for (int b = 0; b < m; ++b) {
+      float s = 0.f;
+#pragma unroll
+      for (int a = 0; a < m; ++a) s += Kc[a] * Quu[a][b];
+      KcQuu[b] = s;
+    }
+    float Vr[n];
+#pragma unroll
+    for (int kk = 0; kk < n; ++kk) {
+      float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        s1 += Q[n + a] * K[a][kk];
+        s2 += Kc[a] * Qux[a][kk];
+        s3 += KcQuu[a] * K[a][kk];
+      }
+      Vr[kk] = ((Q[kk] + s1) + s2) + s3;
+    }
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      s1 += Q[n + a] * k[a];
+      s2 += Kc[a] * qu[a];
+      s3 += KcQuu[a] * k[a];
+    }
+    float vr = ((qr + s1) + s2) + s3;
+    // every lane has finished reading the old V (first barrier above)
+#pragma unroll
+    for (int kk = 0; kk < n; ++kk) L.V[r][kk] = Vr[kk];
+    L.v[r] = vr;
+  }
+}
+
+// standalone sweep, F from HBM (the LinDx / classic path and the north-star
+// kernel for rocket shapes)
+template <int n, int m, int MODE>
+__global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const float* __restrict__ C,
+                                                           const float* __restrict__ c, const float* __restrict__ x,
+                                                           const float* __restrict__ u, const float* __restrict__ F,
+                                                           Bounds bd, const unsigned char* __restrict__ zI,
+                                                           float* __restrict__ K, float* __restrict__ k,
+                                                           int* __restrict__ n_qp) {
+  constexpr int d = n + m;
+  __shared__ GroupLds<n, m> Ls[kGPW];
+  const int r = threadIdx.x & (kG - 1);
+  const int gp = threadIdx.x / kG;
+  const int b = blockIdx.x * kGPW + gp;
+  const bool valid = b < B;
+  const int bb = valid ? b : 0;
+  GroupLds<n, m>& L = Ls[gp];
+  if (r < n) {
+#pragma unroll
+    for (int kk = 0; kk < GroupLds<n, m>::W; ++kk) L.V[r][kk] = 0.f;
+    L.v[r] = 0.f;
+  }
+  float prev_k[m];
+#pragma unroll
+  for (int a = 0; a < m; ++a) prev_k[a] = 0.f;
+  bool have_prev = false;
+  int nqp = 0;
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t tb = (size_t)t * B + bb;
+    float Crow[d], cb = 0.f, tau_r = 0.f;
+#pragma unroll
+    for (int j = 0; j < d; ++j) Crow[j] = 0.f;
+    if (r < d) {
+      ld(Crow, C + (tb * d + r) * d);
+      cb = c[tb * d + r];
+      if (x) tau_r = r < n ? x[tb * n + r] : u[tb * m + (r - n)];
+    }
+    if (r < n) {
+      if (t < T - 1) {
+        float Fr[d];
+        ld(Fr, F + (tb * n + r) * d);
+#pragma unroll
+        for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < d; ++j) L.F[r][j] = 0.f;
+      }
+    }
+    if (r < d) L.tau[r] = tau_r;
+    __syncthreads();
+    if (x && r < d) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < d; ++j) s += Crow[j] * L.tau[j];
+      cb = s + cb;
+    }
+    float zIt[m], lb[m], ub[m], ut[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      ut[a] = u ? u[tb * m + a] : 0.f;
+      zIt[a] = (MODE == GAIN_ZERO_I && zI[tb * m + a]) ? 1.f : 0.f;
+      lb[a] = ub[a] = 0.f;
+      if constexpr (MODE == GAIN_BOX) {
+        lb[a] = bound_lo(bd, tb * m + a) - ut[a];
+        ub[a] = bound_hi(bd, tb * m + a) - ut[a];
+      }
+    }
+    float Kt[m][n], kt[m];
+    group_riccati_step<n, m, MODE>(L, r, Crow, cb, zIt, lb, ub, Kt, kt, prev_k, have_prev, nqp);
+    if (valid) {
+      if (r < n) {
+#pragma unroll
+        for (int a = 0; a < m; ++a) K[tb * m * n + a * n + r] = L.Kk[a][r];
+      }
+      if (r < m) k[tb * m + r] = L.Kk[r][GroupLds<n, m>::W];
+    }
+    __syncthreads();
+  }
+  if (valid && n_qp && r == 0) n_qp[b] = nqp;
+}
+
+// ---------------------------------------------------------------- forward pass
+// forward_pass (dilqr_kernels.hip) for a 16-lane group: lane r < n carries
+// state component r, K . dx is a 16-lane shuffle sum, the full state for the
+// dynamics and the stage cost is exchanged through LDS, and the stage cost is
+// shuffle-reduced from the per-row terms tau_r (C_r . tau) / 2 + c_r tau_r.
+// Dynamics: Model::forward_row (model rollout) or, with md == nullptr, the
+// LinDx step x' = F_t tau + f_t with F row r read by lane r.
+template <int n, int m, int GREC, class Model>
+DEV float group_forward_pass(GroupLds<n, m>& L, const Model* md, const float* __restrict__ F,
+                             const float* __restrict__ f, int T, int B, int b, int r, bool valid, float alpha,
+                             const float* __restrict__ x_init, const float* __restrict__ C,
+                             const float* __restrict__ c, const float* __restrict__ x, const float* __restrict__ u,
+                             const float* __restrict__ K, const float* __restrict__ k,
+                             const float* __restrict__ grec, const Bounds& bd, const unsigned char* __restrict__ zI,
+                             float* __restrict__ x_out, float* __restrict__ u_out, float* __restrict__ du_sq,
+                             float* old_cost_out) {
+  constexpr int d = n + m;
+  float xr = (r < n) ? x_init[(size_t)b * n + r] : 0.f;      // this lane's state component
+  float dxr = 0.f;
+  if (valid && r < n) x_out[(size_t)b * n + r] = xr;
+  float cst = 0.f, oldc = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const size_t tb = (size_t)t * B + b;
+    float ut[m], kt[m], Kc[m];
+    if constexpr (GREC > 0) {
+      const float* rec = grec + tb * GREC;
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        kt[a] = rec[m * n + a];
+        Kc[a] = r < n ? rec[a * n + r] : 0.f;
+      }
+      oldc += rec[m * n + m];
+    } else {
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        kt[a] = k[tb * m + a];
+        Kc[a] = r < n ? K[(tb * m + a) * n + r] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < m; ++a) ut[a] = u[tb * m + a];
+    float nu[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      float s = group_sum(Kc[a] * dxr);
+      nu[a] = (s + ut[a]) + alpha * kt[a];
+      if (zI && zI[tb * m + a]) nu[a] = 0.f;
+      if (bd.mode != DILQR_BOUNDS_NONE) nu[a] = eclamp(nu[a], bound_lo(bd, tb * m + a), bound_hi(bd, tb * m + a));
+    }
+    float nur = 0.f, uur = 0.f;
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      nur = (r == n + a) ? nu[a] : nur;
+      uur = (r == n + a) ? ut[a] : uur;
+    }
+    if (valid && r >= n && r < d) {
+      u_out[tb * m + (r - n)] = nur;
+      if (du_sq) {
+        float e = uur - nur;
+        du_sq[((size_t)t * m + (r - n)) * B + b] = e * e;
+      }
+    }
+    // the full new state through LDS
+    if (r < n) L.tau[r] = xr;
+    __syncthreads();
+    float xf[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) xf[i] = L.tau[i];
+    __syncthreads();
+    const float taur = r < n ? xr : nur;
+    float part = 0.f;
+    if (r < d) {
+      float Crow[d];
+      ld(Crow, C + (tb * d + r) * d);
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < n; ++j) s += Crow[j] * xf[j];
+#pragma unroll
+      for (int a = 0; a < m; ++a) s += Crow[n + a] * nu[a];
+      part = 0.5f * (taur * s) + taur * c[tb * d + r];
+    }
+    cst += group_sum(part);                                  // all 16 lanes shuffle
+    if (t < T - 1 && r < n) {
+      float xnext;
+      if constexpr (std::is_same_v<Model, GroupNoModel>) {
+        float Fr[d];
+        ld(Fr, F + (tb * n + r) * d);
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += Fr[j] * xf[j];
+#pragma unroll
+        for (int a = 0; a < m; ++a) s += Fr[n + a] * nu[a];
+        xnext = f ? s + f[tb * n + r] : s;
+      } else {
+        xnext = md->forward_row(r, xf, nu);
+      }
+      dxr = xnext - x[(tb + B) * n + r];
+      xr = xnext;
+      if (valid) x_out[(tb + B) * n + r] = xr;
+    }
+  }
+  if (old_cost_out) *old_cost_out = oldc;
+  return cst;
+}
+
+// the line search's accept test (lqr_step_explicit.py:244-252) for a group.  The
+// 16 lanes of a group hold the same cost, so `done` is group-uniform; the wave
+// keeps looping until every group accepted (its barriers stay balanced), and a
+// group that already accepted re-runs its pass at the same alpha, reproducing
+// the same trajectory.  Returns true when the wave may leave the loop.
+DEV bool group_ls_done(float cost, float old_cost, int ls, int max_ls, bool valid, float& alpha, float decay) {
+  const bool done = !(cost > old_cost) || ls == max_ls - 1;
+  if (__all(done || !valid)) return true;
+  if (!done) alpha *= decay;
+  return false;
+}
+
+// current trajectory cost (lqr_step_explicit.py:171) for a group
+template <int n, int m>
+DEV float group_traj_cost(int T, int B, int b, int r, const float* __restrict__ C, const float* __restrict__ c,
+                          const float* __restrict__ x, const float* __restrict__ u) {
+  constexpr int d = n + m;
+  float cost = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const size_t tb = (size_t)t * B + b;
+    float part = 0.f;
+    if (r < d) {
+      float xt[n], ut[m], Crow[d];
+      ld(xt, x + tb * n); ld(ut, u + tb * m); ld(Crow, C + (tb * d + r) * d);
+      float s = 0.f, taur = 0.f;
+#pragma unroll
+      for (int j = 0; j < n; ++j) { s += Crow[j] * xt[j]; taur = (j == r) ? xt[j] : taur; }
+#pragma unroll
+      for (int a = 0; a < m; ++a) { s += Crow[n + a] * ut[a]; taur = (r == n + a) ? ut[a] : taur; }
+      part = 0.5f * (taur * s) + taur * c[tb * d + r];
+    }
+    cost += group_sum(part);
+  }
+  return cost;
+}
+
+// standalone line search (lqr_forward, lqr_step_explicit.py:166-263) for a group
+template <int n, int m, class Model>
+__global__ void __launch_bounds__(64) k_lqr_forward_group(int T, int B, const float* __restrict__ theta,
+                                                          const float* __restrict__ F, const float* __restrict__ f,
+                                                          const float* __restrict__ x_init,
+                                                          const float* __restrict__ C, const float* __restrict__ c,
+                                                          const float* __restrict__ x, const float* __restrict__ u,
+                                                          const float* __restrict__ K, const float* __restrict__ k,
+                                                          Bounds bd, const unsigned char* __restrict__ zI,
+                                                          float decay, int max_ls, float* __restrict__ x_out,
+                                                          float* __restrict__ u_out, float* __restrict__ cost_out,
+                                                          float* __restrict__ du_sq, float* __restrict__ alpha_out) {
+  __shared__ GroupLds<n, m> Ls[kGPW];
+  const int r = threadIdx.x & (kG - 1);
+  const int gp = threadIdx.x / kG;
+  const int b0 = blockIdx.x * kGPW + gp;
+  const bool valid = b0 < B;
+  const int b = valid ? b0 : B - 1;
+  Model md;
+  if constexpr (!std::is_same_v<Model, GroupNoModel>) md.load(theta);
+  const float old_cost = group_traj_cost<n, m>(T, B, b, r, C, c, x, u);
+  float alpha = 1.f, cost = 0.f;
+  for (int ls = 0; ls < max_ls; ++ls) {
+    cost = group_forward_pass<n, m, 0>(Ls[gp], &md, F, f, T, B, b, r, valid, alpha, x_init, C, c, x, u, K, k,
+                                       nullptr, bd, zI, x_out, u_out, ls == 0 ? du_sq : nullptr, nullptr);
+    if (group_ls_done(cost, old_cost, ls, max_ls, valid, alpha, decay)) break;
+  }
+  if (valid && r == 0) {
+    cost_out[b] = cost;
+    if (alpha_out) alpha_out[b] = alpha;
+  }
+}
+
+// ---------------------------------------------------------------- fused iteration
+// ilqr_problem (dilqr_kernels.hip) for a 16-lane group: on-the-fly Jacobian
+// rows (Model::jac_row), Riccati + stage costs, gain records, line-search rollout
+// with row-distributed dynamics (Model::deriv) and shuffle-reduced costs.
+template <class Model, int MODE>
+DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r, bool valid,
+                            const Model& md, const float* __restrict__ x_init, const float* __restrict__ C,
+                            const float* __restrict__ c, const float* __restrict__ x, const float* __restrict__ u,
+                            const Bounds& bd, float decay, int max_ls, float* __restrict__ ws,
+                            float* __restrict__ x_out, float* __restrict__ u_out, float* __restrict__ du_sq,
+                            float& cost_out, float& alpha_out) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
+  constexpr int W = GroupLds<n, m>::W;
+  // ---------------- backward
+  if (r < n) {
+#pragma unroll
+    for (int kk = 0; kk < W; ++kk) L.V[r][kk] = 0.f;
+    L.v[r] = 0.f;
+  }
+  float prev_k[m];
+#pragma unroll
+  for (int a = 0; a < m; ++a) prev_k[a] = 0.f;
+  bool have_prev = false;
+  int nqp = 0;
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t tb = (size_t)t * B + b;
+    float Crow[d], cr = 0.f, xt[n], ut[m];
+    ld(xt, x + tb * n);                              // the group's 16 lanes read the same 64 B
+    ld(ut, u + tb * m);
+#pragma unroll
+    for (int j = 0; j < d; ++j) Crow[j] = 0.f;
+    if (r < d) { ld(Crow, C + (tb * d + r) * d); cr = c[tb * d + r]; }
+    if (r < n) {
+      float Fr[d];
+      if (t < T - 1) {
+        md.jac_row(r, xt, ut, Fr);
+      } else {
+#pragma unroll
+        for (int j = 0; j < d; ++j) Fr[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
+    }
+    __syncthreads();
+    float tau[d];
+#pragma unroll
+    for (int i = 0; i < n; ++i) tau[i] = xt[i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+    float Ct = 0.f;
+#pragma unroll
+    for (int j = 0; j < d; ++j) Ct += Crow[j] * tau[j];
+    float taur = 0.f;
+#pragma unroll
+    for (int j = 0; j < d; ++j) taur = (j == r) ? tau[j] : taur;
+    const float obj = group_sum(r < d ? 0.5f * (taur * Ct) + taur * cr : 0.f);
+    const float cb = Ct + cr;
+    float zIt[m], lb[m], ub[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      zIt[a] = 0.f; lb[a] = ub[a] = 0.f;
+      if constexpr (MODE == GAIN_BOX) {
+        lb[a] = bound_lo(bd, tb * m + a) - ut[a];
+        ub[a] = bound_hi(bd, tb * m + a) - ut[a];
+      }
+    }
+    float Kt[m][n], kt[m];
+    group_riccati_step<n, m, MODE>(L, r, Crow, cb, zIt, lb, ub, Kt, kt, prev_k, have_prev, nqp);
+    if (valid) {
+      float* rec = ws + tb * GREC;
+      if (r < n) {
+#pragma unroll
+        for (int a = 0; a < m; ++a) rec[a * n + r] = L.Kk[a][r];
+      }
+      if (r < m) rec[m * n + r] = L.Kk[r][W];
+      if (r == m) rec[m * n + m] = obj;
+    }
+    __syncthreads();
+  }
+  // ---------------- forward line search
+  float alpha = 1.f, cost = 0.f, old_cost = 0.f;
+  for (int ls = 0; ls < max_ls; ++ls) {
+    float oldc;
+    cost = group_forward_pass<n, m, GREC>(L, &md, nullptr, nullptr, T, B, b, r, valid, alpha, x_init, C, c, x, u,
+                                          nullptr, nullptr, ws, bd, nullptr, x_out, u_out, ls == 0 ? du_sq : nullptr,
+                                          &oldc);
+    if (ls == 0) old_cost = oldc;
+    if (group_ls_done(cost, old_cost, ls, max_ls, valid, alpha, decay)) break;
+  }
+  cost_out = cost;
+  alpha_out = alpha;
+}
+
+}  // namespace dilqr

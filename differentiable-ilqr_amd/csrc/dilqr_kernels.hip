@@ -17,6 +17,11 @@ static inline int grid_for(long long n) { return (int)((n + kBlock - 1) / kBlock
 
 DEV float bound_lo(const Bounds& bd, long long idx) { return bd.mode == DILQR_BOUNDS_TENSOR ? bd.lo_t[idx] : bd.lo; }
 DEV float bound_hi(const Bounds& bd, long long idx) { return bd.mode == DILQR_BOUNDS_TENSOR ? bd.hi_t[idx] : bd.hi; }
+}  // namespace dilqr
+
+#include "dilqr_group.h"   // 16-lanes-per-problem kernels (rocket-sized d <= 16)
+
+namespace dilqr {
 
 // ============================================================ model kernels
 template <class Model>
@@ -587,23 +592,110 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   S.slot[b] = (unsigned char)nw;
 }
 
+// the same two kernels for the 16-lanes-per-problem models (dilqr_group.h)
+template <class Model, int MODE>
+__global__ void __launch_bounds__(64) k_ilqr_iterate_group(int T, int B, const float* __restrict__ theta,
+                                                           const float* __restrict__ x_init,
+                                                           const float* __restrict__ C, const float* __restrict__ c,
+                                                           const float* __restrict__ x, const float* __restrict__ u,
+                                                           Bounds bd, float decay, int max_ls, float* __restrict__ ws,
+                                                           float* __restrict__ x_out, float* __restrict__ u_out,
+                                                           float* __restrict__ cost_out, float* __restrict__ du_sq,
+                                                           float* __restrict__ alpha_out,
+                                                           const dilqr_mpc_ctrl* __restrict__ ctrl) {
+  __shared__ GroupLds<Model::N, Model::M> Ls[kGPW];
+  if (ctrl && ctrl->stopped) return;
+  const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
+  const int b0 = blockIdx.x * kGPW + gp;
+  const bool valid = b0 < B;
+  const int b = valid ? b0 : B - 1;          // idle groups shadow problem B-1 (same wave), writing nothing
+  Model md; md.load(theta);
+  float cost, alpha;
+  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, x, u, bd, decay, max_ls, ws, x_out,
+                                  u_out, du_sq, cost, alpha);
+  if (valid && r == 0) {
+    cost_out[b] = cost;
+    alpha_out[b] = alpha;
+  }
+}
+
+template <class Model, int MODE>
+__global__ void __launch_bounds__(64) k_mpc_iterate_group(int T, int B, const float* __restrict__ theta,
+                                                          const float* __restrict__ x_init,
+                                                          const float* __restrict__ C, const float* __restrict__ c,
+                                                          Bounds bd, float decay, int max_ls, int first,
+                                                          float best_cost_eps, MpcState S) {
+  constexpr int n = Model::N, m = Model::M;
+  __shared__ GroupLds<n, m> Ls[kGPW];
+  if (S.ctrl->stopped) return;
+  const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
+  const int b0 = blockIdx.x * kGPW + gp;
+  const bool valid = b0 < B;
+  const int b = valid ? b0 : B - 1;
+  Model md; md.load(theta);
+  const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
+  const int cur = S.slot[b], best = S.slot[B + b];
+  const int nw = (cur != 0 && best != 0) ? 0 : ((cur != 1 && best != 1) ? 1 : 2);
+  float cost, alpha;
+  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, S.X3 + cur * TBn, S.U3 + cur * TBm,
+                                  bd, decay, max_ls, S.ws, S.X3 + nw * TBn, S.U3 + nw * TBm, S.du_sq, cost, alpha);
+  if (valid && r == 0) {
+    S.cost[b] = cost;
+    S.alpha[b] = alpha;
+    const bool better = !first && (cost <= S.best_cost[b] + best_cost_eps);   // mpc_explicit.py:278
+    if (first || better) {
+      S.best_cost[b] = cost;
+      S.slot[B + b] = (unsigned char)nw;
+    }
+    S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
+    S.slot[b] = (unsigned char)nw;
+  }
+}
+
 // full_du_norm (the reference's batch-mixing rows), best_du for the problems
 // that took this iterate, then — in the last workgroup to finish — the stop
 // rule (mpc_explicit.py:264, 279, 297-299).  Cross-workgroup hand-off: every
 // workgroup's contributions are device-scope atomics; a release fence before and
 // an acquire fence after the arrival counter make them visible to the last one.
+template <bool STAGE>
 __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float eps, int not_improved_lim,
                                                           MpcState S) {
+  // the block's rows are one contiguous span of TM*256 floats: stage it through
+  // LDS with coalesced loads, then each thread sums its row (stride TM words;
+  // TM odd -> conflict-free, TM even -> at most 2-way)
+  extern __shared__ __attribute__((aligned(16))) float sdu[];
   __shared__ unsigned red_max[4];
   __shared__ int red_any[4];
   __shared__ int last;
   if (S.ctrl->stopped) return;
   int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (STAGE) {
+    const size_t base = (size_t)blockIdx.x * blockDim.x * TM;
+    const size_t total = (size_t)B * TM;
+    const int span = blockDim.x * TM;
+    // 8 independent loads in flight per thread before the first LDS store
+    // (a load->store loop would serialise one HBM latency per element)
+    constexpr int U = 8;
+    for (int i0 = threadIdx.x; i0 < span; i0 += blockDim.x * U) {
+      float v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int i = i0 + j * blockDim.x;
+        v[j] = (i < span && base + i < total) ? S.du_sq[base + i] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int i = i0 + j * blockDim.x;
+        if (i < span) sdu[i] = v[j];
+      }
+    }
+  }
+  if constexpr (STAGE) __syncthreads();
   unsigned mx = 0u;
   int any = 0;
   if (r < B) {
     float s = 0.f;
-    const float* p = S.du_sq + (size_t)r * TM;
+    const float* p = STAGE ? sdu + (size_t)threadIdx.x * TM : S.du_sq + (size_t)r * TM;
     for (int i = 0; i < TM; ++i) s += p[i];
     float fdn = sqrtf(s);
     S.full_du_norm[r] = fdn;
@@ -1249,6 +1341,23 @@ inline bool bad_bounds(const dilqr_bounds& b) {
 // (n, m) shapes compiled for the generic (LinDx / Riccati / adjoint) kernels.
 // Model kernels use their own fixed shapes.
 #define DILQR_FOR_EACH_SHAPE(X) X(3, 1) X(5, 1) X(4, 3) X(4, 1) X(2, 1) X(4, 2) X(6, 2)
+// shapes served by the 16-lanes-per-problem kernels (dilqr_group.h)
+#define DILQR_FOR_EACH_GROUP_SHAPE(X) X(13, 3)
+#define DILQR_FOR_ALL_SHAPES(X) DILQR_FOR_EACH_SHAPE(X) DILQR_FOR_EACH_GROUP_SHAPE(X)
+
+// the stop-rule kernel with its rows staged in LDS when a block's span fits
+// (64 KiB), else read in place
+inline int launch_norm_control(int TM, int B, float eps, int not_improved_lim, const MpcState& st,
+                               hipStream_t stream) {
+  int threads = 256;
+  while (threads > 64 && (size_t)threads * TM * sizeof(float) > 65536) threads >>= 1;
+  const size_t lds = (size_t)threads * TM * sizeof(float);
+  if (lds <= 65536)
+    k_mpc_norm_control<true><<<(B + threads - 1) / threads, threads, lds, stream>>>(TM, B, eps, not_improved_lim, st);
+  else
+    k_mpc_norm_control<false><<<(B + 255) / 256, 256, 0, stream>>>(TM, B, eps, not_improved_lim, st);
+  return launched();
+}
 
 }  // namespace
 
@@ -1260,16 +1369,28 @@ int dilqr_model_num_params(int model) {
   switch (model) {
     case DILQR_MODEL_PENDULUM: return Pendulum::P;
     case DILQR_MODEL_CARTPOLE: return Cartpole::P;
+    case DILQR_MODEL_ROCKET: return Rocket::P;
     default: return -1;
   }
 }
 
+// every model (per-problem kernels whose state fits a lane: dynamics,
+// Jacobians, rollouts)
 #define MODEL_SWITCH(model, CALL)                       \
+  switch (model) {                                      \
+    case DILQR_MODEL_PENDULUM: { using MD = Pendulum; CALL; break; } \
+    case DILQR_MODEL_CARTPOLE: { using MD = Cartpole; CALL; break; } \
+    case DILQR_MODEL_ROCKET: { using MD = Rocket; CALL; break; }     \
+    default: return DILQR_E_SHAPE;                      \
+  }
+// models whose Riccati state fits one lane (thread-per-problem kernels)
+#define MODEL_SWITCH_TPP(model, CALL)                   \
   switch (model) {                                      \
     case DILQR_MODEL_PENDULUM: { using MD = Pendulum; CALL; break; } \
     case DILQR_MODEL_CARTPOLE: { using MD = Cartpole; CALL; break; } \
     default: return DILQR_E_SHAPE;                      \
   }
+static inline int grid_group(long long B) { return (int)((B + kGPW - 1) / kGPW); }
 
 int dilqr_dynamics_f32(int model, int N, const float* theta, const float* x, const float* u, float* out,
                        void* stream) {
@@ -1296,7 +1417,7 @@ int dilqr_rollout_f32(int model, int n, int m, int T, int B, const float* theta,
     if (!F && T > 1) return DILQR_E_ARG;
 #define X(N_, M_) \
     if (n == N_ && m == M_) { k_rollout_lin<N_, M_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, F, f, x_init, u, x_out); return launched(); }
-    DILQR_FOR_EACH_SHAPE(X)
+    DILQR_FOR_ALL_SHAPES(X)
 #undef X
     return DILQR_E_SHAPE;
   }
@@ -1340,6 +1461,11 @@ int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const flo
     return launched();                                         \
   }
   DILQR_FOR_EACH_SHAPE(X)
+#undef LAUNCH
+#define LAUNCH(N_, M_, MODE_)                                                                                     \
+  k_lqr_backward_group<N_, M_, MODE_><<<grid_group(B), 64, 0, S(stream)>>>(T, B, C, c, x, u, F, bd, u_zero_I, K, k, \
+                                                                           n_qp_iter)
+  DILQR_FOR_EACH_GROUP_SHAPE(X)
 #undef X
 #undef LAUNCH
   return DILQR_E_SHAPE;
@@ -1368,10 +1494,26 @@ int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* th
     }
     DILQR_FOR_EACH_SHAPE(X)
 #undef X
+#define X(N_, M_)                                                                                             \
+    if (n == N_ && m == M_) {                                                                                  \
+      k_lqr_forward_group<N_, M_, GroupNoModel><<<grid_group(B), 64, 0, S(stream)>>>(                          \
+          T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter,     \
+          x_out, u_out, cost, du_sq, alpha);                                                                   \
+      return launched();                                                                                       \
+    }
+    DILQR_FOR_EACH_GROUP_SHAPE(X)
+#undef X
     return DILQR_E_SHAPE;
   }
   if (!theta) return DILQR_E_ARG;
-  MODEL_SWITCH(model, ({
+  if (model == DILQR_MODEL_ROCKET) {
+    if (n != Rocket::N || m != Rocket::M) return DILQR_E_SHAPE;
+    k_lqr_forward_group<Rocket::N, Rocket::M, Rocket><<<grid_group(B), 64, 0, S(stream)>>>(
+        T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter, x_out,
+        u_out, cost, du_sq, alpha);
+    return launched();
+  }
+  MODEL_SWITCH_TPP(model, ({
     if (n != MD::N || m != MD::M) return DILQR_E_SHAPE;
     k_lqr_forward<MD::N, MD::M, MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
         T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter, x_out,
@@ -1401,7 +1543,18 @@ int dilqr_ilqr_iterate_f32(int model, int T, int B, const float* theta, const fl
   if (B == 0) return 0;
   Bounds bd = mkb(bounds);
   bool box = bounds.mode != DILQR_BOUNDS_NONE;
-  MODEL_SWITCH(model, ({
+  if (model == DILQR_MODEL_ROCKET) {
+    if (box)
+      k_ilqr_iterate_group<Rocket, GAIN_BOX><<<grid_group(B), 64, 0, S(stream)>>>(
+          T, B, theta, x_init, C, c, x, u, bd, linesearch_decay, max_linesearch_iter, ws_gains, x_out, u_out, cost,
+          du_sq, alpha, ctrl);
+    else
+      k_ilqr_iterate_group<Rocket, GAIN_UNC><<<grid_group(B), 64, 0, S(stream)>>>(
+          T, B, theta, x_init, C, c, x, u, bd, linesearch_decay, max_linesearch_iter, ws_gains, x_out, u_out, cost,
+          du_sq, alpha, ctrl);
+    return launched();
+  }
+  MODEL_SWITCH_TPP(model, ({
     if (box)
       k_ilqr_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(
           T, B, theta, x_init, C, c, x, u, bd, linesearch_decay, max_linesearch_iter, ws_gains, x_out, u_out, cost,
@@ -1431,7 +1584,7 @@ int dilqr_mpc_update_best_f32(int n, int m, int T, int B, int first, float best_
                                                                 best_du, ctrl);                           \
       ok = true;                                                                                          \
     }
-    DILQR_FOR_EACH_SHAPE(X)
+    DILQR_FOR_ALL_SHAPES(X)
 #undef X
     if (!ok) return DILQR_E_SHAPE;
     int e = launched();
@@ -1490,7 +1643,7 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta, con
   if (bad_bounds(bounds)) return DILQR_E_ARG;
   if (B == 0) return 0;
   Bounds bd = mkb(bounds);
-  MODEL_SWITCH(model, (k_implicit_backward<MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
+  MODEL_SWITCH_TPP(model, (k_implicit_backward<MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
                           T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta)));
   return launched();
 }
@@ -1519,7 +1672,15 @@ int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const flo
   Bounds bd = mkb(bounds);
   bool box = bounds.mode != DILQR_BOUNDS_NONE;
   int m_ = 0;
-  MODEL_SWITCH(model, ({
+  if (model == DILQR_MODEL_ROCKET) {
+    m_ = Rocket::M;
+    if (box)
+      k_mpc_iterate_group<Rocket, GAIN_BOX><<<grid_group(B), 64, 0, S(stream)>>>(
+          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, first, best_cost_eps, st);
+    else
+      k_mpc_iterate_group<Rocket, GAIN_UNC><<<grid_group(B), 64, 0, S(stream)>>>(
+          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, first, best_cost_eps, st);
+  } else MODEL_SWITCH_TPP(model, ({
     m_ = MD::M;
     if (box)
       k_mpc_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, bd,
@@ -1532,8 +1693,7 @@ int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const flo
   }));
   int e = launched();
   if (e) return e;
-  k_mpc_norm_control<<<(B + 255) / 256, 256, 0, S(stream)>>>(T * m_, B, eps, not_improved_lim, st);
-  return launched();
+  return launch_norm_control(T * m_, B, eps, not_improved_lim, st, S(stream));
 }
 
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out, float* u_out,
@@ -1542,7 +1702,7 @@ int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, fl
   if (B == 0) return 0;
 #define X(N_, M_) \
   if (n == N_ && m == M_) { k_mpc_gather<N_, M_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, st, x_out, u_out); return launched(); }
-  DILQR_FOR_EACH_SHAPE(X)
+  DILQR_FOR_ALL_SHAPES(X)
 #undef X
   return DILQR_E_SHAPE;
 }

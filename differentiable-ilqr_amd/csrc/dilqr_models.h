@@ -137,3 +137,132 @@ template <class Model> struct D2Of;
 template <> struct D2Of<Pendulum> { using type = gen::PendulumD2; static constexpr bool XX00_ZERO = false; };
 template <> struct D2Of<Cartpole> { using type = gen::CartpoleD2; static constexpr bool XX00_ZERO = true; };
 }  // namespace dilqr
+
+namespace dilqr {
+// ---------------------------------------------------------------- rocket
+// env_dx/rocket.py: x = [r(3), v(3), q(4), w(3)], u = thrust (3), theta =
+// (Jx, Jy, Jz, mass, l), dt = 0.1.  The reference returns the UNNORMALISED
+// quaternion (rocket.py:159-164: new_x_out is built but new_x is returned).
+struct Rocket {
+  static constexpr int N = 13, M = 3, P = 5;
+  static constexpr float DT = 0.1f;
+  float Jx, Jy, Jz, mass, l;
+  DEV void load(const float* __restrict__ th) { Jx = th[0]; Jy = th[1]; Jz = th[2]; mass = th[3]; l = th[4]; }
+
+  struct FSparsity {    // rocket.py:324-426 (69 nonzeros)
+    static constexpr bool nz(int i, int j) {
+      return i == j || (i < 3 && j == i + 3) || (i >= 3 && i < 6 && j >= 6 && j <= 9) ||
+             (i >= 3 && i < 6 && j >= 13) || (i >= 6 && i < 10 && j >= 6 && j <= 12) ||
+             (i >= 10 && j >= 10 && j <= 12) || (i == 11 && j == 15) || (i == 12 && j == 14);
+    }
+  };
+
+  // derivative of state component r (rocket.py:94-156), contraction off so the
+  // rounding follows the reference's eager ops
+  DEV float deriv(int r, const float (&x)[N], const float (&u)[M]) const {
+#pragma clang fp contract(off)
+    const float q0 = x[6], q1 = x[7], q2 = x[8], q3 = x[9], wx = x[10], wy = x[11], wz = x[12];
+    const float Tx = fminf(fmaxf(u[0], -400.f), 400.f);
+    const float Ty = fminf(fmaxf(u[1], -400.f), 400.f);
+    const float Tz = fminf(fmaxf(u[2], -400.f), 400.f);
+    switch (r) {
+      case 0: case 1: case 2: return x[3 + r];
+      case 3: return (((1.f - 2.f * (q2 * q2 + q3 * q3)) * Tx + 2.f * (q1 * q2 - q0 * q3) * Ty) +
+                      2.f * (q1 * q3 + q0 * q2) * Tz) / mass + -10.f;
+      case 4: return ((2.f * (q1 * q2 + q0 * q3) * Tx + (1.f - 2.f * (q1 * q1 + q3 * q3)) * Ty) +
+                      2.f * (q2 * q3 - q0 * q1) * Tz) / mass + 0.f;
+      case 5: return ((2.f * (q1 * q3 - q0 * q2) * Tx + 2.f * (q2 * q3 + q0 * q1) * Ty) +
+                      (1.f - 2.f * (q1 * q1 + q2 * q2)) * Tz) / mass + 0.f;
+      case 6: return 0.5f * (((-wx * q1) + (-wy * q2)) + (-wz * q3));
+      case 7: return 0.5f * (((wx * q0) + (wz * q2)) + (-wy * q3));
+      case 8: return 0.5f * (((wy * q0) + (-wz * q1)) + (wx * q3));
+      case 9: return 0.5f * (((wz * q0) + (wy * q1)) + (-wx * q2));
+      case 10: return (1.f / Jx) * (0.f - (wy * (Jz * wz) - wz * (Jy * wy)));
+      case 11: return (1.f / Jy) * ((l / 2.f) * Tz - (wz * (Jx * wx) - wx * (Jz * wz)));
+      default: return (1.f / Jz) * (-(l / 2.f) * Ty - (wx * (Jy * wy) - wy * (Jx * wx)));
+    }
+  }
+
+  DEV void forward(const float (&x)[N], const float (&u)[M], float (&o)[N]) const {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int r = 0; r < N; ++r) o[r] = x[r] + deriv(r, x, u) * DT;
+  }
+  // component r of forward() (the 16-lanes-per-problem kernels, dilqr_group.h)
+  DEV float forward_row(int r, const float (&x)[N], const float (&u)[M]) const {
+#pragma clang fp contract(off)
+    return x[r] + deriv(r, x, u) * DT;
+  }
+
+  // row r of get_linear_dyn (rocket.py:324-426), unclamped u
+  DEV void jac_row(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M]) const {
+    const float dt = DT;
+    const float q0 = x[6], q1 = x[7], q2 = x[8], q3 = x[9], wx = x[10], wy = x[11], wz = x[12];
+    const float ux = u[0], uy = u[1], uz = u[2];
+#pragma unroll
+    for (int j = 0; j < N + M; ++j) D[j] = (j == r) ? 1.f : 0.f;
+    switch (r) {
+      case 0: case 1: case 2: D[r + 3] = dt; break;
+      case 3:
+        D[6] = dt * (uz * 2 * q2 - uy * 2 * q3) / mass;
+        D[7] = dt * (uy * 2 * q2 + uz * 2 * q3) / mass;
+        D[8] = dt * (uy * 2 * q1 - ux * 4 * q2 + uz * 2 * q0) / mass;
+        D[9] = dt * (uz * 2 * q1 - ux * 4 * q3 - uy * 2 * q0) / mass;
+        D[13] = dt * (1 - 2 * (q2 * q2 + q3 * q3)) / mass;
+        D[14] = dt * 2 * (q1 * q2 - q0 * q3) / mass;
+        D[15] = dt * 2 * (q1 * q3 + q0 * q2) / mass;
+        break;
+      case 4:
+        D[6] = dt * (ux * 2 * q3 - uz * 2 * q1) / mass;
+        D[7] = dt * (ux * 2 * q2 - uy * 4 * q1 - uz * 2 * q0) / mass;
+        D[8] = dt * (ux * 2 * q1 + uz * 2 * q3) / mass;
+        D[9] = dt * (ux * 2 * q0 - uy * 4 * q3 + uz * 2 * q2) / mass;
+        D[13] = dt * 2 * (q1 * q2 + q0 * q3) / mass;
+        D[14] = dt * (1 - 2 * (q1 * q1 + q3 * q3)) / mass;
+        D[15] = dt * 2 * (q2 * q3 - q0 * q1) / mass;
+        break;
+      case 5:
+        D[6] = dt * (uy * 2 * q1 - ux * 2 * q2) / mass;
+        D[7] = dt * (ux * 2 * q3 + uy * 2 * q0 - uz * 4 * q1) / mass;
+        D[8] = dt * (uy * 2 * q3 - ux * 2 * q0 - uz * 4 * q2) / mass;
+        D[9] = dt * (ux * 2 * q1 + uy * 2 * q2) / mass;
+        D[13] = dt * 2 * (q1 * q3 - q0 * q2) / mass;
+        D[14] = dt * 2 * (q2 * q3 + q0 * q1) / mass;
+        D[15] = dt * (1 - 2 * (q1 * q1 + q2 * q2)) / mass;
+        break;
+      case 6:
+        D[7] = -dt * 0.5f * wx; D[8] = -dt * 0.5f * wy; D[9] = -dt * 0.5f * wz;
+        D[10] = -dt * 0.5f * q1; D[11] = -dt * 0.5f * q2; D[12] = -dt * 0.5f * q3;
+        break;
+      case 7:
+        D[6] = dt * 0.5f * wx; D[8] = dt * 0.5f * wz; D[9] = -dt * 0.5f * wy;
+        D[10] = dt * 0.5f * q0; D[11] = -dt * 0.5f * q3; D[12] = dt * 0.5f * q2;
+        break;
+      case 8:
+        D[6] = dt * 0.5f * wy; D[7] = -dt * 0.5f * wz; D[9] = dt * 0.5f * wx;
+        D[10] = dt * 0.5f * q3; D[11] = dt * 0.5f * q0; D[12] = -dt * 0.5f * q1;
+        break;
+      case 9:
+        D[6] = dt * 0.5f * wz; D[7] = dt * 0.5f * wy; D[8] = -dt * 0.5f * wx;
+        D[10] = -dt * 0.5f * q2; D[11] = dt * 0.5f * q1; D[12] = dt * 0.5f * q0;
+        break;
+      case 10:
+        D[11] = -dt * (wz * Jz - wz * Jy) / Jx; D[12] = -dt * (wy * Jz - wy * Jy) / Jx;
+        break;
+      case 11:
+        D[10] = -dt * (wz * Jx - wz * Jz) / Jy; D[12] = -dt * (wx * Jx - wx * Jz) / Jy;
+        D[15] = dt * (l / 2) / Jy;
+        break;
+      default:  // 12
+        D[10] = -dt * (wy * Jy - wy * Jx) / Jz; D[11] = -dt * (wx * Jy - wx * Jx) / Jz;
+        D[14] = -dt * (l / 2) / Jz;
+        break;
+    }
+  }
+
+  DEV void jacobian(const float (&x)[N], const float (&u)[M], float (&D)[N][N + M]) const {
+#pragma unroll
+    for (int r = 0; r < N; ++r) jac_row(r, x, u, D[r]);
+  }
+};
+}  // namespace dilqr

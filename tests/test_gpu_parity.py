@@ -43,11 +43,12 @@ def _need_gpu():
 def dilqr_models():
     from dilqr.env_dx.cartpole import CartpoleDx
     from dilqr.env_dx.pendulum import PendulumDx
-    return {"cartpole": CartpoleDx, "pendulum": PendulumDx}
+    from dilqr.env_dx.rocket import RocketDx
+    return {"cartpole": CartpoleDx, "pendulum": PendulumDx, "rocket": RocketDx}
 
 
 # ------------------------------------------------------------------ dynamics
-@pytest.mark.parametrize("name", ["pendulum", "cartpole"])
+@pytest.mark.parametrize("name", ["pendulum", "cartpole", "rocket"])
 def test_dynamics_and_jacobian(golden, name):
     g = golden("models_f64")
     x, u = g[f"{name}_x"], g[f"{name}_u"]
@@ -122,6 +123,7 @@ MPC_CASES = {
     "cart_il": ("cartpole", 25, 40, (-100.0, 100.0), 1e-4, 5, 0.5, 2),
     "pend_unc": ("pendulum", 10, 10, None, 0.0, 10 ** 9, 0.2, 5),
     "pend_box": ("pendulum", 10, 10, (-2.0, 2.0), 0.0, 10 ** 9, 0.2, 5),
+    "rocket_unc": ("rocket", 30, 5, None, 0.0, 10 ** 9, 0.2, 5),
 }
 
 
@@ -337,3 +339,111 @@ def test_implicit_backward_full_size():
                                        c[:, sl].contiguous(), None, None, x[:, sl].contiguous(),
                                        u[:, sl].contiguous(), K[:, sl].contiguous(), -10.0, 10.0, None)
     assert torch.equal(dth[sl], dth2) and torch.equal(dC[:, sl], dC2)
+
+
+# ------------------------------------------------------------------ 16-lanes-per-problem kernels (rocket)
+@pytest.mark.parametrize("variant", ["", "chol_", "zI_", "box_"])
+def test_riccati_group_rocket_vs_golden(golden, variant):
+    """(n,m)=(13,3): the group Riccati sweep against the reference's sweep on the
+    same random LQR (riccati golden, rocket shape).  The bounded case is checked
+    against the per-problem oracle (the reference's pnqp is batch-coupled) and
+    against the golden at a looser bar."""
+    from dilqr import _native as N
+    from dilqr import ops
+    g = golden("riccati_f64")
+    n, m = 13, 3
+    C, c, F, u = g["rocket_C"], g["rocket_c"], g["rocket_F"], g["rocket_u"]
+    kw = {}
+    if variant == "chol_":
+        kw = dict(m_solver=N.SOLVE_CHOL)
+    elif variant == "zI_":
+        kw = dict(u_zero_I=torch.tensor(g["rocket_zI"], device=DEV))
+    elif variant == "box_":
+        kw = dict(u=gpu(u), u_lower=-1.0, u_upper=1.0)
+    K, k, _ = ops.lqr_backward(gpu(C), gpu(c), gpu(F), n, m, **kw)
+    # pnqp's m=3 active-set solves amplify fp32 rounding (measured 1.4e-4 on k)
+    tol = 1e-3 if variant == "box_" else 1e-4
+    if variant == "box_":
+        Ko, ko, _ = olqr.lqr_backward(C, c, F, n, m, u=u, u_lower=-1.0, u_upper=1.0, per_problem=True)
+        assert relerr(cpu(K), Ko) < tol and relerr(cpu(k), ko) < tol
+    assert relerr(cpu(K), g[f"rocket_{variant}K"]) < tol
+    assert relerr(cpu(k), g[f"rocket_{variant}k"]) < tol
+
+
+@pytest.mark.parametrize("dyn", ["rocket", "lindx"])
+@pytest.mark.parametrize("bounds", [None, (-0.5, 0.5)])
+def test_lqr_forward_group_vs_oracle(dyn, bounds):
+    """Group line-search rollout (row-distributed dynamics, shuffle-reduced
+    costs) against the oracle's lqr_forward on one sweep's gains."""
+    from dilqr import ops
+    from dilqr.env_dx.rocket import RocketDx
+    rng = np.random.RandomState(5)
+    n, m, T, B = 13, 3, 30, 37                        # B not a multiple of 4: idle groups
+    M = omodels.Rocket
+    x0 = np.concatenate([rng.uniform(-1, 1, (B, 6)), np.tile([1., 0, 0, 0], (B, 1)) + 0.05 * rng.normal(size=(B, 4)),
+                         rng.normal(0, 0.05, (B, 3))], 1)
+    u = rng.uniform(-0.5, 0.5, (T, B, m))
+    q, p = M.true_obj()
+    C, c = ompc.expand_cost(np.diag(q), p, T, B)
+    if dyn == "rocket":
+        x = olqr.get_traj(T, u, x0, lambda xx, uu: M.forward(xx, uu))
+        F, f = ompc.linearize(M, x, u)
+        odyn = lambda xx, uu: M.forward(xx, uu)
+    else:
+        F = rng.normal(0, 0.03, (T, B, n, n + m)); F[..., :n] += 0.9 * np.eye(n)
+        f = rng.normal(0, 0.1, (T, B, n))
+        x = olqr.get_traj(T, u, x0, ("lin", F, f))
+        odyn = ("lin", F, f)
+    cb = olqr.c_back(C, c, x, u)
+    lo, hi = bounds if bounds else (None, None)
+    Ko, ko, _ = olqr.lqr_backward(C, cb, F, n, m, u=u, u_lower=lo, u_upper=hi, per_problem=True)
+    xo, uo, co, *_ = olqr.lqr_forward(x0, C, c, x, u, Ko, ko, odyn, u_lower=lo, u_upper=hi,
+                                     linesearch_decay=0.2, max_linesearch_iter=5)
+    dx = RocketDx()
+    mid = dx.model_id if dyn == "rocket" else 0
+    nx, nu, cost, _, _ = ops.lqr_forward(mid, ops.theta_of(dx, gpu(x0)), gpu(x0), gpu(C), gpu(c), gpu(x), gpu(u),
+                                         gpu(Ko), gpu(ko), F=gpu(F), f=gpu(f), u_lower=lo, u_upper=hi,
+                                         linesearch_decay=0.2, max_linesearch_iter=5)
+    assert relerr(cpu(cost), co) < 1e-4
+    assert relerr(cpu(nu), uo) < 1e-3
+    assert relerr(cpu(nx), xo) < 1e-3
+
+
+def test_rocket_fused_iteration_equals_unfused(golden):
+    g = golden("mpc_f64")
+    mname, T, it, bounds, eps, nil, decay, mls = MPC_CASES["rocket_unc"]
+    x0 = g["rocket_unc_x0"]
+    a = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls, fused=True)
+    b = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls, fused=False)
+    for ta, tb in zip(a, b):
+        assert relerr(cpu(ta), cpu(tb)) < 1e-3
+
+
+def test_rocket_mpc_full_size_batch_independence():
+    """Config 3 shape (B=32768, T=30): a solve over the whole batch returns, for
+    a sample of problems, what solving those problems alone returns."""
+    import dilqr
+    from dilqr.env_dx.rocket import RocketDx
+    T, B = 30, 32768
+    rng = np.random.RandomState(3)
+    x0 = np.concatenate([rng.uniform([0, -4, -2.5], [10, 4, 2.5], (B, 3)), rng.normal(0, 0.1, (B, 3)),
+                         np.tile([1., 0, 0, 0], (B, 1)) + 0.05 * rng.normal(size=(B, 4)),
+                         rng.normal(0, 0.02, (B, 3))], 1)
+    dx = RocketDx()
+    q, p = dx.get_true_obj()
+
+    def solve(xs):
+        Bs = xs.shape[0]
+        C = torch.diag(q).repeat(T, Bs, 1, 1).to(DEV)
+        c = p.repeat(T, Bs, 1).to(DEV)
+        mpc = dilqr.MPC(13, 3, T, lqr_iter=5, eps=0.0, not_improved_lim=10 ** 9, linesearch_decay=0.2,
+                        max_linesearch_iter=5, exit_unconverged=False, detach_unconverged=False)
+        with torch.no_grad():
+            return mpc(gpu(xs), dilqr.QuadCost(C, c), dx)
+
+    x, u, cost = solve(x0)
+    assert torch.isfinite(cost).all()
+    idx = np.array([0, 1, 4097, 12345, B - 1])
+    xs, us, cs = solve(x0[idx])
+    assert relerr(cpu(cost[idx]), cpu(cs)) < 1e-5
+    assert relerr(cpu(u[:, idx]), cpu(us)) < 1e-4
