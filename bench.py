@@ -80,6 +80,142 @@ def cpu_baseline(budget_s=12.0, sample=2048):
                       f"in {dt:.1f}s, fp64, 1 thread"}
 
 
+def _timed_solves(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, lqr_iter, solves, warmup_solves):
+    """Whole fixed-iteration solves (eps=0, not_improved_lim=inf) -> (problem-iters/s, ms/iteration)."""
+    from dilqr import _native as N
+
+    def solve():
+        sv.begin(model_id, theta, x0)
+        for i in range(lqr_iter):
+            sv.iterate(model_id, theta, x0, C, c, bounds, decay, max_ls, i == 0, 1e-4, 0.0, 10 ** 9)
+    for _ in range(warmup_solves):
+        solve()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(solves):
+        solve()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert bool(torch.isfinite(sv.best_cost).all()), "non-finite costs"
+    del N
+    return sv.B * lqr_iter * solves / dt, dt * 1e3 / (lqr_iter * solves)
+
+
+def _event_ms(stream, fn, reps):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for r in range(reps):
+        ev[r][0].record(stream)
+        fn(r)
+        ev[r][1].record(stream)
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def riccati_workload(n, m, T, B, dev, seed=0):
+    """SURVEY.md §8(d) Riccati-kernel roofline workload: C = L L^T + 0.1 I (SPD,
+    distinct per (t,b)), c_back ~ N(0,1), F = [I + 0.05 N | 0.1 N]."""
+    d = n + m
+    g = torch.Generator(device=dev).manual_seed(seed)
+    L = torch.randn(T, B, d, d, device=dev, generator=g) * (0.5 / d ** 0.5)
+    C = (L @ L.transpose(-1, -2) + 0.1 * torch.eye(d, device=dev)).contiguous()
+    del L
+    cb = torch.randn(T, B, d, device=dev, generator=g)
+    F = torch.cat([torch.eye(n, device=dev) + 0.05 * torch.randn(T - 1, B, n, n, device=dev, generator=g),
+                   0.1 * torch.randn(T - 1, B, n, m, device=dev, generator=g)], -1).contiguous()
+    return C, cb, F
+
+
+def sweep_roofline(n, m, T, B, dev, reps=5):
+    """Standalone Riccati sweep (F from HBM) on the synthetic workload."""
+    from dilqr import _native as N
+    C, cb, F = riccati_workload(n, m, T, B, dev)
+    K = torch.empty(T, B, m, n, device=dev)
+    k = torch.empty(T, B, m, device=dev)
+    nb = N.Bounds(N.BOUNDS_NONE, 0.0, 0.0, None, None)
+    s = N.stream(dev)
+    call = lambda r: N.call("dilqr_lqr_backward_f32", n, m, T, B, N.ptr(C), N.ptr(cb), None, None, N.ptr(F), nb,
+                            None, 0, N.ptr(K), N.ptr(k), None, s)
+    call(0)
+    ms = _event_ms(torch.cuda.current_stream(dev), call, reps)
+    d = n + m
+    nbytes = 4 * (T * d * d + T * d + (T - 1) * n * d + T * m * n + T * m) * B
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"shape": [n, m, T, B], "avg_launch_ms": ms, "algorithmic_bytes_per_launch": nbytes,
+            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}
+
+
+def secondary_configs(dev):
+    """BASELINE.json configs 3 and 4 on one GPU (information lines beside the headline)."""
+    from dilqr import _native as N
+    from dilqr import ops
+    from dilqr.implicit import implicit_backward
+    out = {}
+    stream = torch.cuda.current_stream(dev)
+    s = N.stream(dev)
+    # ---- config 3: rocket n=13 m=3 T=30 B=32768, unconstrained, decay 0.2, max_ls 5, lqr_iter 10
+    T, B, n, m = 30, 32768, 13, 3
+    rng = np.random.RandomState(0)
+    r = rng.uniform([0, -4, -2.5], [10, 4, 2.5], (B, 3))
+    v = rng.normal(0, 0.1, (B, 3))
+    q4 = np.array([1., 0, 0, 0]) + 0.05 * rng.normal(size=(B, 4))
+    q4 /= np.linalg.norm(q4, axis=1, keepdims=True)
+    w = rng.normal(0, 0.02, (B, 3))
+    x0 = torch.tensor(np.concatenate([r, v, q4, w], 1), dtype=torch.float32, device=dev)
+    from dilqr.env_dx.rocket import RocketDx
+    dx = RocketDx()
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(dev).contiguous()
+    c = p.repeat(T, B, 1).to(dev).contiguous()
+    theta = ops.theta_of(dx, x0)
+    sv = ops.MPCSolve(T, B, n, m, dev)
+    nb, _ = N.make_bounds(None, None)
+    val, ms_it = _timed_solves(sv, N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, 10, 2, 1)
+    sv.begin(N.MODEL_ROCKET, theta, x0)
+    xa, ua, xb, ub = sv.Xs[0], sv.Us[0], sv.Xs[1], sv.Us[1]
+    call = lambda _r: N.call("dilqr_ilqr_iterate_f32", N.MODEL_ROCKET, T, B, N.ptr(theta), N.ptr(x0), N.ptr(C),
+                             N.ptr(c), N.ptr(xa), N.ptr(ua), nb, 0.2, 5, N.ptr(sv.ws), N.ptr(xb), N.ptr(ub),
+                             N.ptr(sv.cost), N.ptr(sv.du_sq), N.ptr(sv.alpha), None, s)
+    it_ms = _event_ms(stream, call, 5)
+    d = n + m
+    it_bytes = 4 * (T * d * d + T * d + n + 2 * T * d + 2) * B                 # 36,540 B/problem
+    out["config3_rocket"] = {
+        "value": val, "unit": "problem-iters/s", "ms_per_iter": ms_it, "batch": B, "T": T,
+        "fused_iteration": {"kernel": "k_ilqr_iterate_group<Rocket>", "avg_launch_ms": it_ms,
+                            "algorithmic_bytes_per_launch": it_bytes,
+                            "frac": it_bytes / (it_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+        "riccati_sweep": sweep_roofline(n, m, T, B, dev)}
+    del sv, C, c, x0
+    # ---- config 4: cartpole T=25 B=65536 with bounds (+-100 reference value, +-10 stress) + implicit backward
+    T, B, n, m = 25, 65536, 5, 1
+    x0n, qn, pn = make_problems(B)
+    x0 = torch.tensor(x0n, device=dev)
+    C = torch.diag(torch.tensor(qn)).repeat(T, B, 1, 1).to(dev).contiguous()
+    c = torch.tensor(pn).repeat(T, B, 1).to(dev).contiguous()
+    theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
+    sv = ops.MPCSolve(T, B, n, m, dev)
+    for lim in (100.0, 10.0):
+        bd, keep = N.make_bounds(-lim, lim)
+        val, ms_it = _timed_solves(sv, N.MODEL_CARTPOLE, theta, x0, C, c, bd, 0.5, 2, 10, 3, 1)
+        active = float(((sv.gather_best()[1].abs() - lim).abs() < 1e-6).float().mean())
+        out[f"config4_cartpole_box{int(lim)}"] = {"value": val, "unit": "problem-iters/s", "ms_per_iter": ms_it,
+                                                  "batch": B, "T": T, "active_control_frac": active}
+    x, u = sv.gather_best()
+    F, _f = ops.linearize(N.MODEL_CARTPOLE, theta, x, u)
+    K, _k, _ = ops.lqr_backward(C, c, F, n, m, x=x, u=u, u_lower=-10.0, u_upper=10.0)
+    g = torch.Generator(device=dev).manual_seed(1)
+    wx = torch.zeros(T, B, n, device=dev)
+    wu = torch.randn(T, B, m, device=dev, generator=g)                 # loss = sum(u * w), SURVEY §8(d)
+    from dilqr.env_dx.cartpole import CartpoleDx
+    cart = CartpoleDx()
+    ib = lambda _r: implicit_backward(cart, wx, wu, C, c, None, None, x, u, K, -10.0, 10.0, None)
+    ib(0)
+    ms = _event_ms(stream, ib, 5)
+    out["config4_implicit_backward"] = {"kernel": "k_implicit_backward<Cartpole> (dC, dc, dtheta)",
+                                        "avg_ms": ms, "problems_per_s": B / (ms * 1e-3), "batch": B, "T": T,
+                                        "bounds": "+-10"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -88,6 +224,7 @@ def main():
     ap.add_argument("--lqr-iter", type=int, default=10)
     ap.add_argument("--batch", type=int, default=B_PER_GPU, help="problems per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the config 3/4 information lines")
     ap.add_argument("--kernels-only", action="store_true",
                     help="profiling mode: a few launches of the fused iteration and the sweep, no JSON line")
     args = ap.parse_args()
@@ -128,7 +265,7 @@ def main():
         state["i"] += 1
 
     if args.kernels_only:
-        args.steps, args.warmup, args.no_cpu_baseline = 0, 2, True
+        args.steps, args.warmup, args.no_cpu_baseline, args.no_secondary = 0, 2, True, True
     for _ in range(args.warmup):
         step()
     state["i"] = 0
@@ -156,8 +293,8 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     # the fused iteration kernel alone, on the stream it runs on: dilqr_ilqr_iterate_f32 launches the same
     # per-problem body (ilqr_problem) as the slot-based MPC loop, reading/writing plain trajectory buffers
-    xa, ua = sv.X3[0], sv.U3[0]
-    xb, ub = sv.X3[1], sv.U3[1]
+    xa, ua = sv.Xs[0], sv.Us[0]
+    xb, ub = sv.Xs[1], sv.Us[1]
     for r in range(reps):
         ev[r][0].record(stream)
         N.call("dilqr_ilqr_iterate_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C),
@@ -229,6 +366,8 @@ def main():
                                  "frac": sweep_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": sweep_bytes,
                                  "avg_launch_ms": sweep_ms},
         }
+        if world == 1 and not args.no_secondary:
+            line["secondary"] = secondary_configs(dev)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)

@@ -418,11 +418,12 @@ struct FwdIn {
 };
 
 template <class Model, int MODE>
-DEV void ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
-                      const float* __restrict__ C, const float* __restrict__ c, const float* __restrict__ x,
-                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
-                      float* __restrict__ ws, float* __restrict__ x_out, float* __restrict__ u_out,
-                      float* __restrict__ du_sq, float& cost_out, float& alpha_out) {
+DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
+                     const float* __restrict__ C, const float* __restrict__ c, const float* __restrict__ x,
+                     const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
+                     float* __restrict__ ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
+                     float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
+                     float& cost_out, float& alpha_out) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
   constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
   // ---------------- backward: linearise + Riccati + stage costs of the current trajectory
@@ -476,67 +477,102 @@ DEV void ilqr_problem(int T, int B, int b, const Model& md, const float* __restr
       cur = nxt;
     }
   }
-  // ---------------- forward: line-search rollout (lqr_step_explicit.py:166-263)
+  // ---------------- forward: the line search (lqr_step_explicit.py:166-263).
+  // Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
+  // it is the last pass.  Passes 2r and 2r+1 roll out TOGETHER (candidates A
+  // and B), sharing every load of the step; the first accepted candidate wins,
+  // which is exactly the sequential search.  A wave otherwise pays a whole
+  // second latency-bound pass whenever any of its 64 problems backtracks.
   float alpha = 1.f, cost = 0.f, old_cost = 0.f;
-  for (int ls = 0; ls < max_ls; ++ls) {
-    float xn[n], dx[n];
-    ld(xn, x_init + (size_t)b * n);
+  int win = 0;
+  for (int p = 0; p < max_ls; p += 2) {
+    const bool twoB = p + 1 < max_ls;                       // uniform
+    const float aA = alpha, aB = alpha * decay;
+    float xA[n], dA[n], xB[n], dB[n];
+    ld(xA, x_init + (size_t)b * n);
 #pragma unroll
-    for (int i = 0; i < n; ++i) dx[i] = 0.f;
-    st(x_out + (size_t)b * n, xn);
-    float cst = 0.f, oldc = 0.f;
+    for (int i = 0; i < n; ++i) { dA[i] = 0.f; xB[i] = xA[i]; dB[i] = 0.f; }
+    st(xa_out + (size_t)b * n, xA);
+    if (twoB) st(xb_out + (size_t)b * n, xB);
+    float cA = 0.f, cB = 0.f, oldc = 0.f;
     FwdIn<n, m, GREC> cur, nxt;
     cur.load(ws, u, C, c, x, (size_t)b, (size_t)(T > 1 ? 1 : 0) * B + b);
     for (int t = 0; t < T; ++t) {
-      size_t tb = (size_t)t * B + b;
+      const size_t tb = (size_t)t * B + b;
       {
         int t1 = t + 1 < T ? t + 1 : t;                 // prefetch step t+1
         int t2 = t + 2 < T ? t + 2 : t1;
         nxt.load(ws, u, C, c, x, (size_t)t1 * B + b, (size_t)t2 * B + b);
       }
-      float nu[m];
+      float nuA[m], nuB[m];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
-        float s = 0.f;
+        float sA = 0.f, sB = 0.f;
 #pragma unroll
-        for (int j = 0; j < n; ++j) s += cur.g[a * n + j] * dx[j];
-        nu[a] = (s + cur.u[a]) + alpha * cur.g[m * n + a];
-        if (bd.mode != DILQR_BOUNDS_NONE) nu[a] = eclamp(nu[a], bound_lo(bd, tb * m + a), bound_hi(bd, tb * m + a));
+        for (int j = 0; j < n; ++j) {
+          sA += cur.g[a * n + j] * dA[j];
+          sB += cur.g[a * n + j] * dB[j];
+        }
+        nuA[a] = (sA + cur.u[a]) + aA * cur.g[m * n + a];
+        nuB[a] = (sB + cur.u[a]) + aB * cur.g[m * n + a];
+        if (bd.mode != DILQR_BOUNDS_NONE) {
+          const float lo = bound_lo(bd, tb * m + a), hi = bound_hi(bd, tb * m + a);
+          nuA[a] = eclamp(nuA[a], lo, hi);
+          nuB[a] = eclamp(nuB[a], lo, hi);
+        }
       }
       oldc += cur.g[m * n + m];
-      st(u_out + tb * m, nu);
-      if (ls == 0) {
+      st(ua_out + tb * m, nuA);
+      if (twoB) st(ub_out + tb * m, nuB);
+      if (p == 0) {
 #pragma unroll
         for (int a = 0; a < m; ++a) {
-          float e = cur.u[a] - nu[a];
+          float e = cur.u[a] - nuA[a];
           du_sq[((size_t)t * m + a) * B + b] = e * e;
         }
       }
       float tau[d];
 #pragma unroll
-      for (int i = 0; i < n; ++i) tau[i] = xn[i];
+      for (int i = 0; i < n; ++i) tau[i] = xA[i];
 #pragma unroll
-      for (int a = 0; a < m; ++a) tau[n + a] = nu[a];
-      cst += quad_cost(cur.C, cur.c, tau);
+      for (int a = 0; a < m; ++a) tau[n + a] = nuA[a];
+      cA += quad_cost(cur.C, cur.c, tau);
+      if (twoB) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) tau[i] = xB[i];
+#pragma unroll
+        for (int a = 0; a < m; ++a) tau[n + a] = nuB[a];
+        cB += quad_cost(cur.C, cur.c, tau);
+      }
       if (t < T - 1) {
         float xnext[n];
-        md.forward(xn, nu, xnext);
+        md.forward(xA, nuA, xnext);
 #pragma unroll
         for (int i = 0; i < n; ++i) {
-          dx[i] = xnext[i] - cur.xnext[i];
-          xn[i] = xnext[i];
+          dA[i] = xnext[i] - cur.xnext[i];
+          xA[i] = xnext[i];
         }
-        st(x_out + (tb + B) * n, xn);
+        st(xa_out + (tb + B) * n, xA);
+        if (twoB) {
+          md.forward(xB, nuB, xnext);
+#pragma unroll
+          for (int i = 0; i < n; ++i) {
+            dB[i] = xnext[i] - cur.xnext[i];
+            xB[i] = xnext[i];
+          }
+          st(xb_out + (tb + B) * n, xB);
+        }
       }
       cur = nxt;
     }
-    cost = cst;
-    if (ls == 0) old_cost = oldc;
-    if (!(cost > old_cost) || ls == max_ls - 1) break;
-    alpha *= decay;
+    if (p == 0) old_cost = oldc;
+    if (!(cA > old_cost) || p == max_ls - 1) { cost = cA; alpha = aA; win = 0; break; }
+    if (!(cB > old_cost) || p + 1 == max_ls - 1) { cost = cB; alpha = aB; win = 1; break; }
+    alpha = aB * decay;                                     // lqr_step_explicit.py:249
   }
   cost_out = cost;
   alpha_out = alpha;
+  return win;
 }
 
 template <class Model, int MODE>
@@ -551,19 +587,49 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
   if (ctrl && ctrl->stopped) return;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  constexpr int n = Model::N, m = Model::M;
+  constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
   Model md; md.load(theta);
   float cost, alpha;
-  ilqr_problem<Model, MODE>(T, B, b, md, x_init, C, c, x, u, bd, decay, max_ls, ws, x_out, u_out, du_sq, cost,
-                            alpha);
+  // line-search candidate B rolls out into the workspace tail and is copied
+  // over (x_out, u_out) when it wins
+  float* xb = ws + (size_t)T * B * GREC;
+  float* ub = xb + (size_t)T * B * n;
+  const int win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, C, c, x, u, bd, decay, max_ls, ws, x_out, u_out,
+                                            xb, ub, du_sq, cost, alpha);
+  if (win) {
+    for (int t = 0; t < T; ++t) {
+      const size_t tb = (size_t)t * B + b;
+      float xt[n], ut[m];
+      ld(xt, xb + tb * n); ld(ut, ub + tb * m);
+      st(x_out + tb * n, xt); st(u_out + tb * m, ut);
+    }
+  }
   cost_out[b] = cost;
   alpha_out[b] = alpha;
 }
 
 // ---------------- the device-resident MPC loop with per-problem trajectory slots
-// Three trajectory buffers per problem ([3,T,B,n] / [3,T,B,m]); each problem
-// keeps the index of its current and best slot, so "best = this iterate"
-// (mpc_explicit.py:277-283) is an index update, never a copy.
+// Four trajectory buffers per problem ([4,T,B,n] / [4,T,B,m]); each problem
+// keeps the index of its current and best slot, and the line search's two
+// candidates roll out into the two free ones, so "accept candidate" and "best
+// = this iterate" (mpc_explicit.py:277-283) are index updates, never copies.
 using MpcState = dilqr_mpc_state;
+constexpr int kSlots = 4;
+
+// the two lowest slot indices not in {cur, best}
+DEV void free_slots(int cur, int best, int& sa, int& sb) {
+  int k = 0;
+  sa = sb = 0;
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) {
+    if (s != cur && s != best) {
+      if (k == 0) sa = s;
+      else if (k == 1) sb = s;
+      ++k;
+    }
+  }
+}
 
 template <class Model, int MODE>
 __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const float* __restrict__ theta,
@@ -576,11 +642,14 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   if (b >= B) return;
   Model md; md.load(theta);
   const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
-  int cur = S.slot[b], best = S.slot[B + b];
-  int nw = (cur != 0 && best != 0) ? 0 : ((cur != 1 && best != 1) ? 1 : 2);
+  const int cur = S.slot[b], best = S.slot[B + b];
+  int sa, sb;
+  free_slots(cur, best, sa, sb);
   float cost, alpha;
-  ilqr_problem<Model, MODE>(T, B, b, md, x_init, C, c, S.X3 + cur * TBn, S.U3 + cur * TBm, bd, decay, max_ls, S.ws,
-                            S.X3 + nw * TBn, S.U3 + nw * TBm, S.du_sq, cost, alpha);
+  const int win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, C, c, S.Xs + cur * TBn, S.Us + cur * TBm, bd,
+                                            decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
+                                            S.Us + sb * TBm, S.du_sq, cost, alpha);
+  const int nw = win ? sb : sa;
   S.cost[b] = cost;
   S.alpha[b] = alpha;
   bool better = !first && (cost <= S.best_cost[b] + best_cost_eps);      // mpc_explicit.py:278
@@ -635,10 +704,11 @@ __global__ void __launch_bounds__(64) k_mpc_iterate_group(int T, int B, const fl
   Model md; md.load(theta);
   const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
   const int cur = S.slot[b], best = S.slot[B + b];
-  const int nw = (cur != 0 && best != 0) ? 0 : ((cur != 1 && best != 1) ? 1 : 2);
+  int nw, unused;
+  free_slots(cur, best, nw, unused);
   float cost, alpha;
-  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, S.X3 + cur * TBn, S.U3 + cur * TBm,
-                                  bd, decay, max_ls, S.ws, S.X3 + nw * TBn, S.U3 + nw * TBm, S.du_sq, cost, alpha);
+  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, S.Xs + cur * TBn, S.Us + cur * TBm,
+                                  bd, decay, max_ls, S.ws, S.Xs + nw * TBn, S.Us + nw * TBm, S.du_sq, cost, alpha);
   if (valid && r == 0) {
     S.cost[b] = cost;
     S.alpha[b] = alpha;
@@ -756,14 +826,14 @@ __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float*
   S.slot[b] = 0; S.slot[B + b] = 0;
   float xt[n];
   ld(xt, x_init + (size_t)b * n);
-  st(S.X3 + (size_t)b * n, xt);
+  st(S.Xs + (size_t)b * n, xt);
   for (int t = 0; t < T - 1; ++t) {
     float ut[m], xn[n];
-    ld(ut, S.U3 + ((size_t)t * B + b) * m);
+    ld(ut, S.Us + ((size_t)t * B + b) * m);
     md.forward(xt, ut, xn);
 #pragma unroll
     for (int i = 0; i < n; ++i) xt[i] = xn[i];
-    st(S.X3 + ((size_t)(t + 1) * B + b) * n, xt);
+    st(S.Xs + ((size_t)(t + 1) * B + b) * n, xt);
   }
 }
 
@@ -773,8 +843,8 @@ __global__ void __launch_bounds__(kBlock) k_mpc_gather(int T, int B, MpcState S,
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   int best = S.slot[B + b];
-  const float* X = S.X3 + (size_t)best * T * B * n;
-  const float* U = S.U3 + (size_t)best * T * B * m;
+  const float* X = S.Xs + (size_t)best * T * B * n;
+  const float* U = S.Us + (size_t)best * T * B * m;
   for (int t = 0; t < T; ++t) {
     size_t tb = (size_t)t * B + b;
     float xt[n], ut[m];
@@ -1650,8 +1720,8 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta, con
 
 
 static bool bad_state(const dilqr_mpc_state& st) {
-  return !st.X3 || !st.U3 || !st.slot || !st.best_cost || !st.best_du || !st.improved || !st.cost || !st.alpha ||
-         !st.du_sq || !st.full_du_norm || !st.ws || !st.ctrl || !st.done_counter || !al16(st.X3) || !al16(st.U3) ||
+  return !st.Xs || !st.Us || !st.slot || !st.best_cost || !st.best_du || !st.improved || !st.cost || !st.alpha ||
+         !st.du_sq || !st.full_du_norm || !st.ws || !st.ctrl || !st.done_counter || !al16(st.Xs) || !al16(st.Us) ||
          !al16(st.ws);
 }
 

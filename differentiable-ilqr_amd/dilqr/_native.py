@@ -31,7 +31,7 @@ CTRL_INTS = 8          # sizeof(dilqr_mpc_ctrl) / 4
 class MpcState(ctypes.Structure):
     """dilqr_mpc_state: device pointers of one MPC solve (include/dilqr.h)."""
     _fields_ = [(name, ctypes.c_void_p) for name in
-                ("X3", "U3", "slot", "best_cost", "best_du", "improved", "cost", "alpha", "du_sq",
+                ("Xs", "Us", "slot", "best_cost", "best_du", "improved", "cost", "alpha", "du_sq",
                  "full_du_norm", "ws", "ctrl", "done_counter")]
 
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float

@@ -104,6 +104,12 @@ def grec_floats(n, m):
     return ((m * n + m + 1) + 3) // 4 * 4
 
 
+def ilqr_ws_floats(n, m):
+    """Per-(t,b) workspace of dilqr_ilqr_iterate_f32: gain record + the line
+    search's second candidate (x, u)."""
+    return grec_floats(n, m) + n + m
+
+
 class MPCWorkspace:
     """Device buffers of one MPC solve (reused across iterations)."""
 
@@ -127,13 +133,14 @@ class MPCWorkspace:
 
 class MPCSolve:
     """Device state of one fused MPC solve (dilqr_mpc_state): three trajectory
-    slots per problem, per-problem best bookkeeping, the loop control block."""
+    slots per problem (current, best, two line-search candidates), per-problem
+    best bookkeeping, the loop control block."""
 
     def __init__(self, T, B, n, m, device):
         dev = device
         self.T, self.B, self.n, self.m = T, B, n, m
-        self.X3 = torch.empty(3, T, B, n, device=dev)
-        self.U3 = torch.zeros(3, T, B, m, device=dev)
+        self.Xs = torch.empty(4, T, B, n, device=dev)
+        self.Us = torch.zeros(4, T, B, m, device=dev)
         self.slot = torch.zeros(2, B, dtype=torch.uint8, device=dev)
         self.best_cost = torch.empty(B, device=dev)
         self.best_du = torch.empty(B, device=dev)
@@ -142,22 +149,22 @@ class MPCSolve:
         self.alpha = torch.empty(B, device=dev)
         self.du_sq = torch.empty(T, m, B, device=dev)
         self.full_du_norm = torch.empty(B, device=dev)
-        self.ws = torch.empty(T * B * grec_floats(n, m), device=dev)
+        self.ws = torch.empty(T * B * ilqr_ws_floats(n, m), device=dev)
         self.ctrl = torch.zeros(N.CTRL_INTS, dtype=torch.int32, device=dev)
         self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
         self.state = N.MpcState(*[t.data_ptr() for t in (
-            self.X3, self.U3, self.slot, self.best_cost, self.best_du, self.improved, self.cost, self.alpha,
+            self.Xs, self.Us, self.slot, self.best_cost, self.best_du, self.improved, self.cost, self.alpha,
             self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter)])
 
     def begin(self, model_id, theta, x_init, u_init=None):
         """x = get_traj(u_init or 0) into slot 0; reset slots and the control block."""
         if u_init is None:
-            self.U3[0].zero_()
+            self.Us[0].zero_()
         else:
-            u0 = u_init.to(device=self.U3.device, dtype=torch.float32)
+            u0 = u_init.to(device=self.Us.device, dtype=torch.float32)
             if u0.ndimension() == 2:
                 u0 = u0.unsqueeze(1).expand(self.T, self.B, self.m)
-            self.U3[0].copy_(u0)
+            self.Us[0].copy_(u0)
         N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), self.state,
                N.stream(x_init.device))
 
@@ -168,8 +175,8 @@ class MPCSolve:
                int(min(not_improved_lim, 2 ** 31 - 1)), self.state, N.stream(x_init.device))
 
     def gather_best(self):
-        x = torch.empty(self.T, self.B, self.n, device=self.X3.device)
-        u = torch.empty(self.T, self.B, self.m, device=self.X3.device)
+        x = torch.empty(self.T, self.B, self.n, device=self.Xs.device)
+        u = torch.empty(self.T, self.B, self.m, device=self.Xs.device)
         N.call("dilqr_mpc_gather_best_f32", self.n, self.m, self.T, self.B, self.state, N.ptr(x), N.ptr(u),
                N.stream(x.device))
         return x, u

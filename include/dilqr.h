@@ -139,8 +139,10 @@ typedef struct dilqr_mpc_ctrl {
 /* One fused iLQR iteration for a model (not LINDX): linearise on the fly,
    Riccati sweep (+pnqp), old cost, line-search rollout.  Reads the current
    trajectory (x,u), writes the new one (x_out,u_out), cost [B], du_sq [T,m,B],
-   alpha [B].  ws_gains: workspace of T*B*(m*n+m) floats.  No-op when
-   ctrl->stopped. */
+   alpha [B].  The line search rolls passes 2r and 2r+1 out together and keeps
+   the first accepted (the sequential search's result).  ws_gains: workspace
+   of T*B*(ceil4(m*n+m+1) + n + m) floats (gain records + the second
+   candidate's trajectory).  No-op when ctrl->stopped. */
 int dilqr_ilqr_iterate_f32(int model, int T, int B, const float* theta,
                            const float* x_init, const float* C, const float* c,
                            const float* x, const float* u, dilqr_bounds bounds,
@@ -189,18 +191,19 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
                                 float* dC, float* dc, float* dtheta, void* stream);
 
 /* ---- the device-resident MPC loop with per-problem trajectory slots ------ */
-/* Caller-owned device buffers of one solve.  X3 [3,T,B,n] and U3 [3,T,B,m] hold
-   three trajectories per problem; slot [2,B] (uint8) the indices of each
-   problem's current and best one, so taking an iterate as the new best
-   (mpc_explicit.py:277-283) moves no data.  ws: T*B*ceil4(m*n+m+1) floats.
-   done_counter: one uint (zeroed by begin). */
+/* Caller-owned device buffers of one solve.  Xs [4,T,B,n] and Us [4,T,B,m] hold
+   four trajectories per problem; slot [2,B] (uint8) the indices of each
+   problem's current and best one.  The line search's two candidates roll out
+   into the two free slots, so accepting a step size or taking an iterate as
+   the new best (mpc_explicit.py:277-283) moves no data.
+   ws: T*B*ceil4(m*n+m+1) floats.  done_counter: one uint (zeroed by begin). */
 typedef struct dilqr_mpc_state {
-  float* X3; float* U3; unsigned char* slot; float* best_cost; float* best_du;
+  float* Xs; float* Us; unsigned char* slot; float* best_cost; float* best_du;
   int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;
   float* ws; dilqr_mpc_ctrl* ctrl; unsigned* done_counter;
 } dilqr_mpc_state;
 
-/* Start a solve: x = get_traj(u) from the controls the caller placed in U3
+/* Start a solve: x = get_traj(u) from the controls the caller placed in Us
    slot 0 (zeros or u_init), slots/ctrl reset (mpc_explicit.py:228-249). */
 int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init,
                         dilqr_mpc_state st, void* stream);

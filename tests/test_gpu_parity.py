@@ -447,3 +447,69 @@ def test_rocket_mpc_full_size_batch_independence():
     xs, us, cs = solve(x0[idx])
     assert relerr(cpu(cost[idx]), cpu(cs)) < 1e-5
     assert relerr(cpu(u[:, idx]), cpu(us)) < 1e-4
+
+
+# ------------------------------------------------------------------ standalone fused iteration
+@pytest.mark.parametrize("model,bounds,decay,mls", [("cartpole", None, 0.5, 2), ("cartpole", (-10.0, 10.0), 0.5, 2),
+                                                    ("pendulum", None, 0.2, 5), ("pendulum", None, 0.2, 3)])
+def test_fused_iteration_vs_oracle(model, bounds, decay, mls):
+    """dilqr_ilqr_iterate_f32 (on-the-fly linearisation, Riccati, line search
+    with passes rolled out in pairs) against the oracle's sequential
+    linearize -> lqr_backward -> lqr_forward, from the trajectory of a few oracle
+    MPC iterations (near convergence, where problems backtrack)."""
+    from dilqr import _native as N
+    from dilqr import ops
+    M = omodels.MODELS[model]
+    n, m = M.n_state, M.n_ctrl
+    T, B = (25, 192) if model == "cartpole" else (10, 192)
+    rng = np.random.RandomState(7)
+    if model == "cartpole":
+        th = rng.uniform(-np.pi, np.pi, B)
+        x0 = np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                       rng.uniform(-1, 1, B)], 1)
+    else:
+        th = rng.uniform(-np.pi / 2, np.pi / 2, B)
+        x0 = np.stack([np.cos(th), np.sin(th), rng.uniform(-1, 1, B)], 1)
+    q, p = M.true_obj()
+    C, c = ompc.expand_cost(np.diag(q), p, T, B)
+    dyn = lambda xx, uu: M.forward(xx, uu)
+    lo, hi = bounds if bounds else (None, None)
+    x, u, _, _ = ompc.mpc_forward(M, x0, C, c, T, u_lower=lo, u_upper=hi, lqr_iter=8, eps=0.0,
+                                  not_improved_lim=10 ** 9, linesearch_decay=decay, max_linesearch_iter=mls,
+                                  per_problem=True)
+    F, f = ompc.linearize(M, x, u)
+    Ko, ko, _ = olqr.lqr_backward(C, olqr.c_back(C, c, x, u), F, n, m, u=u, u_lower=lo, u_upper=hi,
+                                  per_problem=True)
+    xo, uo, co, _, _, _, ao = olqr.lqr_forward(x0, C, c, x, u, Ko, ko, dyn, u_lower=lo, u_upper=hi,
+                                               linesearch_decay=decay, max_linesearch_iter=mls)
+    assert np.any(ao < 1)                      # candidate B / later rounds are exercised
+    th_ = torch.tensor(M.default_params, dtype=torch.float32, device=DEV)
+    Cg, cg, xg, ug, x0g = gpu(C), gpu(c), gpu(x), gpu(u), gpu(x0)
+    ws = torch.empty(T * B * ops.ilqr_ws_floats(n, m), device=DEV)
+    nx, nu = torch.empty_like(xg), torch.empty_like(ug)
+    cost, alpha = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    du_sq = torch.empty(T, m, B, device=DEV)
+    bd, keep = N.make_bounds(lo, hi)
+    mid = {"cartpole": N.MODEL_CARTPOLE, "pendulum": N.MODEL_PENDULUM}[model]
+    N.call("dilqr_ilqr_iterate_f32", mid, T, B, N.ptr(th_), N.ptr(x0g), N.ptr(Cg), N.ptr(cg), N.ptr(xg), N.ptr(ug),
+           bd, float(decay), int(mls), N.ptr(ws), N.ptr(nx), N.ptr(nu), N.ptr(cost), N.ptr(du_sq), N.ptr(alpha),
+           None, N.stream(xg.device))
+    torch.cuda.synchronize()
+    # decisions whose margin |cost_p - old| is below fp32 resolution may flip;
+    # every problem whose accept/reject margins are clear must match exactly
+    old = olqr.quad_cost_terms(C, c, np.concatenate([x, u], -1)).sum(0)
+    clear = np.ones(B, bool)
+    a_p = 1.0
+    for p_ in range(mls):
+        _, _, cp, *_ = olqr.lqr_forward(x0, C, c, x, u, Ko, a_p * ko, dyn, u_lower=lo, u_upper=hi,
+                                        max_linesearch_iter=1)
+        reached = ao <= a_p * (1 + 1e-9)               # problems that evaluated pass p
+        clear &= ~reached | (np.abs(cp - old) > 1e-5 * np.maximum(1.0, np.abs(old)))
+        a_p *= decay
+    assert np.mean(clear) > 0.5
+    same = np.abs(cpu(alpha) - ao) < 1e-6 * np.maximum(1, ao)
+    assert same[clear].all(), np.flatnonzero(clear & ~same)
+    cerr = np.abs(cpu(cost) - co) / np.maximum(1.0, np.abs(co))
+    assert np.median(cerr[same]) < 1e-5 and np.max(cerr[same]) < 1e-3
+    assert relerr(cpu(nu)[:, same], uo[:, same]) < 1e-3
+    assert relerr(cpu(nx)[:, same], xo[:, same]) < 1e-3

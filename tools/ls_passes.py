@@ -1,0 +1,30 @@
+"""How many line-search passes does each wave of the headline workload run?
+(the wave runs the max over its 64 problems)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "differentiable-ilqr_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from dilqr import _native as N  # noqa: E402
+from dilqr import ops  # noqa: E402
+
+dev = torch.device("cuda", 0)
+T, B = 25, 65536
+x0n, q, p = bench.make_problems(B)
+x0 = torch.tensor(x0n, device=dev)
+C = torch.diag(torch.tensor(q)).repeat(T, B, 1, 1).to(dev).contiguous()
+c = torch.tensor(p).repeat(T, B, 1).to(dev).contiguous()
+theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
+sv = ops.MPCSolve(T, B, 5, 1, dev)
+nb, _ = N.make_bounds(None, None)
+sv.begin(N.MODEL_CARTPOLE, theta, x0)
+for i in range(10):
+    sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, i == 0, 1e-4, 0.0, 10 ** 9)
+    a = sv.alpha.view(-1, 64)
+    passes = (a < 1).float()
+    print(f"iter {i}: problems with 2 passes {float(passes.mean()):.3f}, waves with 2 passes "
+          f"{float(passes.max(1).values.mean()):.3f}")
