@@ -85,7 +85,7 @@ def _timed_solves(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, lqr_iter
     from dilqr import _native as N
 
     def solve():
-        sv.begin(model_id, theta, x0)
+        sv.begin(model_id, theta, x0, None, C, c)
         for i in range(lqr_iter):
             sv.iterate(model_id, theta, x0, C, c, bounds, decay, max_ls, i == 0, 1e-4, 0.0, 10 ** 9)
     for _ in range(warmup_solves):
@@ -260,7 +260,7 @@ def main():
     def step():
         first = state["i"] % args.lqr_iter == 0
         if first:
-            sv.begin(N.MODEL_CARTPOLE, theta, x0)
+            sv.begin(N.MODEL_CARTPOLE, theta, x0, None, C, c)
         sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, first, 1e-4, 0.0, 10 ** 9)
         state["i"] += 1
 
@@ -286,26 +286,22 @@ def main():
         elapsed = float(tt.item())
     assert bool(torch.isfinite(sv.best_cost).all()), "non-finite costs"
 
-    # ---- roofline of the dominant kernel: the fused iteration, timed with
-    # events on ITS stream (the current stream, where ops launch it)
+    # ---- roofline of the dominant kernel: the fused MPC iteration kernel
+    # (k_mpc_iterate), timed with HIP events on ITS stream (the current stream,
+    # where ops launch it); the stop-rule kernel runs outside the events
     reps = 10
-    sv.begin(N.MODEL_CARTPOLE, theta, x0)
+    sv.begin(N.MODEL_CARTPOLE, theta, x0, None, C, c)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    # the fused iteration kernel alone, on the stream it runs on: dilqr_ilqr_iterate_f32 launches the same
-    # per-problem body (ilqr_problem) as the slot-based MPC loop, reading/writing plain trajectory buffers
-    xa, ua = sv.Xs[0], sv.Us[0]
-    xb, ub = sv.Xs[1], sv.Us[1]
     for r in range(reps):
         ev[r][0].record(stream)
-        N.call("dilqr_ilqr_iterate_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C),
-               N.ptr(c), N.ptr(xa), N.ptr(ua), bounds, 0.5, 2, N.ptr(sv.ws), N.ptr(xb), N.ptr(ub),
-               N.ptr(sv.cost), N.ptr(sv.du_sq), N.ptr(sv.alpha), None, s)
+        N.call("dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C), N.ptr(c),
+               bounds, 0.5, 2, int(r == 0), 1e-4, sv.state, s)
         ev[r][1].record(stream)
-        xa, xb = xb, xa
-        ua, ub = ub, ua
+        N.call("dilqr_mpc_stop_rule_f32", T_HORIZON, N_CTRL, B, 0.0, 10 ** 9, sv.state, s)
     torch.cuda.synchronize(dev)
     iter_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     iter_bytes = ITER_BYTES_PER_PROBLEM * B
+    xa, ua = sv.gather_best()
 
     # standalone Riccati sweep (the north-star's >=50% HBM target kernel)
     F, _f = ops.linearize(N.MODEL_CARTPOLE, theta, xa, ua)
@@ -327,7 +323,7 @@ def main():
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmc_path)).get("k_ilqr_iterate_bytes_per_launch")
+            traffic = json.load(open(pmc_path)).get("k_mpc_iterate_bytes_per_launch")
             traffic = None if traffic is None else traffic * B / B_PER_GPU
         except Exception:
             traffic = None
@@ -357,7 +353,8 @@ def main():
                        "batch_per_gpu": B, "global_batch": B_total, "T": T_HORIZON,
                        "parallelism": f"batch-sharded x{world} (no collective)",
                        "batch_iters_per_s": world * args.steps / elapsed},
-            "roofline": {"kernel": "k_ilqr_iterate<Cartpole> (fused linearise+Riccati+line search)",
+            "roofline": {"kernel": "k_mpc_iterate<Cartpole,UNC> (fused linearise+Riccati+line search, "
+                                   "packed symmetric cost)",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": iter_bytes, "avg_launch_ms": iter_ms},

@@ -396,13 +396,45 @@ __global__ void __launch_bounds__(kBlock) k_quirk_norm(int TM, int B, const floa
 // Latency: at B=65536 there is one wave per SIMD, so every loop software-
 // pipelines its HBM loads one step ahead in registers (the step t-1 / t+1
 // record is in flight while step t computes).
+// Where the fused kernels read the stage cost from: the caller's C [T,B,d,d] and
+// c [T,B,d], or the solve's packed copy (symmetric C: upper triangle row-major,
+// then c, padded to a multiple of 4 floats per (t,b); dilqr_mpc_begin_f32 builds
+// it once per solve when every C_t,b is bitwise symmetric).  Both fill the same
+// full registers, so the arithmetic is identical.
+template <int d>
+struct CostFull {
+  const float* __restrict__ C;
+  const float* __restrict__ c;
+  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t tb) const { ld2(Cr, C + tb * d * d); ld(cr, c + tb * d); }
+};
+
+template <int d>
+constexpr int packed_cost_floats() { return ((d * (d + 1) / 2 + d) + 3) / 4 * 4; }
+
+template <int d>
+struct CostPacked {
+  const float* __restrict__ P;
+  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t tb) const {
+    constexpr int PK = packed_cost_floats<d>();
+    float buf[PK];
+    ld(buf, P + tb * PK);
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < d; ++i)
+#pragma unroll
+      for (int j = i; j < d; ++j) { Cr[i][j] = buf[k]; Cr[j][i] = buf[k]; ++k; }
+#pragma unroll
+    for (int i = 0; i < d; ++i) cr[i] = buf[k++];
+  }
+};
+
 template <int n, int m>
 struct SweepIn {
   static constexpr int d = n + m;
   float C[d][d], c[d], x[n], u[m];
-  DEV void load(const float* __restrict__ Cp, const float* __restrict__ cp, const float* __restrict__ xp,
-                const float* __restrict__ up, size_t tb) {
-    ld2(C, Cp + tb * d * d); ld(c, cp + tb * d); ld(x, xp + tb * n); ld(u, up + tb * m);
+  template <class CostT>
+  DEV void load(const CostT& cs, const float* __restrict__ xp, const float* __restrict__ up, size_t tb) {
+    cs.load(C, c, tb); ld(x, xp + tb * n); ld(u, up + tb * m);
   }
 };
 
@@ -410,16 +442,17 @@ template <int n, int m, int GREC>
 struct FwdIn {
   static constexpr int d = n + m;
   float g[GREC], u[m], C[d][d], c[d], xnext[n];
-  DEV void load(const float* __restrict__ grec, const float* __restrict__ up, const float* __restrict__ Cp,
-                const float* __restrict__ cp, const float* __restrict__ xp, size_t tb, size_t tb1) {
-    ld(g, grec + tb * GREC); ld(u, up + tb * m); ld2(C, Cp + tb * d * d); ld(c, cp + tb * d);
+  template <class CostT>
+  DEV void load(const float* __restrict__ grec, const float* __restrict__ up, const CostT& cs,
+                const float* __restrict__ xp, size_t tb, size_t tb1) {
+    ld(g, grec + tb * GREC); ld(u, up + tb * m); cs.load(C, c, tb);
     ld(xnext, xp + tb1 * n);
   }
 };
 
-template <class Model, int MODE>
-DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
-                     const float* __restrict__ C, const float* __restrict__ c, const float* __restrict__ x,
+template <class Model, int MODE, class CostT>
+DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
+                     const float* __restrict__ x,
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
                      float* __restrict__ ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
                      float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
@@ -431,10 +464,10 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     RiccatiState<n, m> rs;
     rs.init();
     SweepIn<n, m> cur, nxt;
-    cur.load(C, c, x, u, (size_t)(T - 1) * B + b);
+    cur.load(cs, x, u, (size_t)(T - 1) * B + b);
     for (int t = T - 1; t >= 0; --t) {
       size_t tb = (size_t)t * B + b;
-      nxt.load(C, c, x, u, (size_t)(t > 0 ? t - 1 : 0) * B + b);      // prefetch step t-1
+      nxt.load(cs, x, u, (size_t)(t > 0 ? t - 1 : 0) * B + b);        // prefetch step t-1
       float tau[d], Ctau[d], cb[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
@@ -496,13 +529,13 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     if (twoB) st(xb_out + (size_t)b * n, xB);
     float cA = 0.f, cB = 0.f, oldc = 0.f;
     FwdIn<n, m, GREC> cur, nxt;
-    cur.load(ws, u, C, c, x, (size_t)b, (size_t)(T > 1 ? 1 : 0) * B + b);
+    cur.load(ws, u, cs, x, (size_t)b, (size_t)(T > 1 ? 1 : 0) * B + b);
     for (int t = 0; t < T; ++t) {
       const size_t tb = (size_t)t * B + b;
       {
         int t1 = t + 1 < T ? t + 1 : t;                 // prefetch step t+1
         int t2 = t + 2 < T ? t + 2 : t1;
-        nxt.load(ws, u, C, c, x, (size_t)t1 * B + b, (size_t)t2 * B + b);
+        nxt.load(ws, u, cs, x, (size_t)t1 * B + b, (size_t)t2 * B + b);
       }
       float nuA[m], nuB[m];
 #pragma unroll
@@ -595,8 +628,8 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
   // over (x_out, u_out) when it wins
   float* xb = ws + (size_t)T * B * GREC;
   float* ub = xb + (size_t)T * B * n;
-  const int win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, C, c, x, u, bd, decay, max_ls, ws, x_out, u_out,
-                                            xb, ub, du_sq, cost, alpha);
+  const int win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, CostFull<n + m>{C, c}, x, u, bd, decay, max_ls, ws,
+                                            x_out, u_out, xb, ub, du_sq, cost, alpha);
   if (win) {
     for (int t = 0; t < T; ++t) {
       const size_t tb = (size_t)t * B + b;
@@ -646,9 +679,15 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   int sa, sb;
   free_slots(cur, best, sa, sb);
   float cost, alpha;
-  const int win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, C, c, S.Xs + cur * TBn, S.Us + cur * TBm, bd,
-                                            decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
-                                            S.Us + sb * TBm, S.du_sq, cost, alpha);
+  int win;
+  if (S.ctrl->cost_packed)       // uniform: set once per solve by dilqr_mpc_begin_f32
+    win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk}, S.Xs + cur * TBn,
+                                    S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm,
+                                    S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost, alpha);
+  else
+    win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, CostFull<n + m>{C, c}, S.Xs + cur * TBn, S.Us + cur * TBm,
+                                    bd, decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
+                                    S.Us + sb * TBm, S.du_sq, cost, alpha);
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
   S.alpha[b] = alpha;
@@ -813,11 +852,12 @@ __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float e
 // rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl.
 template <class Model>
 __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float* __restrict__ theta,
-                                                      const float* __restrict__ x_init, MpcState S) {
+                                                      const float* __restrict__ x_init, int pack, MpcState S) {
   constexpr int n = Model::N, m = Model::M;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b == 0) {
     dilqr_mpc_ctrl z = {};
+    z.cost_packed = pack ? 1 : 0;      // cleared by k_pack_cost on any asymmetric C
     *S.ctrl = z;
     *S.done_counter = 0u;
   }
@@ -835,6 +875,34 @@ __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float*
     for (int i = 0; i < n; ++i) xt[i] = xn[i];
     st(S.Xs + ((size_t)(t + 1) * B + b) * n, xt);
   }
+}
+
+// the solve's packed cost copy (CostPacked) + the bitwise symmetry check
+template <int d>
+__global__ void __launch_bounds__(256) k_pack_cost(long long TB, const float* __restrict__ C,
+                                                   const float* __restrict__ c, float* __restrict__ P,
+                                                   dilqr_mpc_ctrl* __restrict__ ctrl) {
+  constexpr int PK = packed_cost_floats<d>();
+  const long long tb = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tb >= TB) return;
+  float Cr[d][d], cr[d], buf[PK];
+  ld2(Cr, C + tb * d * d);
+  ld(cr, c + tb * d);
+  bool sym = true;
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < d; ++i)
+#pragma unroll
+    for (int j = i; j < d; ++j) {
+      sym &= __float_as_uint(Cr[i][j]) == __float_as_uint(Cr[j][i]);
+      buf[k++] = Cr[i][j];
+    }
+#pragma unroll
+  for (int i = 0; i < d; ++i) buf[k++] = cr[i];
+#pragma unroll
+  for (; k < PK; ++k) buf[k] = 0.f;
+  st(P + tb * PK, buf);
+  if (__any(!sym) && (threadIdx.x & 63) == 0) atomicExch(&ctrl->cost_packed, 0);
 }
 
 template <int n, int m>
@@ -1435,6 +1503,15 @@ extern "C" {
 
 int dilqr_version(void) { return 1; }
 
+int dilqr_model_num_ctrl(int model) {
+  switch (model) {
+    case DILQR_MODEL_PENDULUM: return Pendulum::M;
+    case DILQR_MODEL_CARTPOLE: return Cartpole::M;
+    case DILQR_MODEL_ROCKET: return Rocket::M;
+    default: return -1;
+  }
+}
+
 int dilqr_model_num_params(int model) {
   switch (model) {
     case DILQR_MODEL_PENDULUM: return Pendulum::P;
@@ -1725,25 +1802,38 @@ static bool bad_state(const dilqr_mpc_state& st) {
          !al16(st.ws);
 }
 
-int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init, dilqr_mpc_state st,
-                        void* stream) {
+int dilqr_mpc_packed_cost_floats(int n, int m) {
+  const int d = n + m;
+  return d < 1 ? -1 : ((d * (d + 1) / 2 + d) + 3) / 4 * 4;
+}
+
+int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
+                        const float* c, dilqr_mpc_state st, void* stream) {
   if (T < 1 || B < 0 || !theta || !x_init || !al16(x_init) || bad_state(st)) return DILQR_E_ARG;
-  MODEL_SWITCH(model, (k_mpc_begin<MD><<<grid_for(B > 0 ? B : 1), kBlock, 0, S(stream)>>>(T, B, theta, x_init, st)));
+  if ((C && !al16(C)) || (c && !al16(c)) || !al16(st.Cpk)) return DILQR_E_ARG;
+  // the packed copy serves the thread-per-problem fused kernels
+  const int pack = (C && c && st.Cpk && B > 0 && model != DILQR_MODEL_ROCKET) ? 1 : 0;
+  MODEL_SWITCH(model, (k_mpc_begin<MD><<<grid_for(B > 0 ? B : 1), kBlock, 0, S(stream)>>>(T, B, theta, x_init, pack,
+                                                                                          st)));
+  if (pack) {
+    int e = launched();
+    if (e) return e;
+    const long long TB = (long long)T * B;
+    MODEL_SWITCH_TPP(model, (k_pack_cost<MD::N + MD::M><<<(int)((TB + 255) / 256), 256, 0, S(stream)>>>(
+                                 TB, C, c, st.Cpk, st.ctrl)));
+  }
   return launched();
 }
 
-int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
-                          const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
-                          int first, float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st,
-                          void* stream) {
+int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
+                       const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
+                       int first, float best_cost_eps, dilqr_mpc_state st, void* stream) {
   if (T < 1 || B < 0 || max_linesearch_iter < 1 || !theta || !x_init || !C || !c) return DILQR_E_ARG;
   if (!al16(x_init) || !al16(C) || !al16(c) || bad_state(st) || bad_bounds(bounds)) return DILQR_E_ARG;
   if (B == 0) return 0;
   Bounds bd = mkb(bounds);
   bool box = bounds.mode != DILQR_BOUNDS_NONE;
-  int m_ = 0;
   if (model == DILQR_MODEL_ROCKET) {
-    m_ = Rocket::M;
     if (box)
       k_mpc_iterate_group<Rocket, GAIN_BOX><<<grid_group(B), 64, 0, S(stream)>>>(
           T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, first, best_cost_eps, st);
@@ -1751,7 +1841,6 @@ int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const flo
       k_mpc_iterate_group<Rocket, GAIN_UNC><<<grid_group(B), 64, 0, S(stream)>>>(
           T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, first, best_cost_eps, st);
   } else MODEL_SWITCH_TPP(model, ({
-    m_ = MD::M;
     if (box)
       k_mpc_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, bd,
                                                                         linesearch_decay, max_linesearch_iter,
@@ -1761,9 +1850,26 @@ int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const flo
                                                                         linesearch_decay, max_linesearch_iter,
                                                                         first, best_cost_eps, st);
   }));
-  int e = launched();
+  return launched();
+}
+
+int dilqr_mpc_stop_rule_f32(int T, int m, int B, float eps, int not_improved_lim, dilqr_mpc_state st,
+                            void* stream) {
+  if (T < 1 || m < 1 || B < 0 || bad_state(st)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  return launch_norm_control(T * m, B, eps, not_improved_lim, st, S(stream));
+}
+
+int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
+                          const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
+                          int first, float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st,
+                          void* stream) {
+  const int m = dilqr_model_num_ctrl(model);
+  if (m < 1) return DILQR_E_SHAPE;
+  int e = dilqr_mpc_step_f32(model, T, B, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter,
+                             first, best_cost_eps, st, stream);
   if (e) return e;
-  return launch_norm_control(T * m_, B, eps, not_improved_lim, st, S(stream));
+  return dilqr_mpc_stop_rule_f32(T, m, B, eps, not_improved_lim, st, stream);
 }
 
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out, float* u_out,

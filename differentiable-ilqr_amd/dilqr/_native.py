@@ -32,12 +32,13 @@ class MpcState(ctypes.Structure):
     """dilqr_mpc_state: device pointers of one MPC solve (include/dilqr.h)."""
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("Xs", "Us", "slot", "best_cost", "best_du", "improved", "cost", "alpha", "du_sq",
-                 "full_du_norm", "ws", "ctrl", "done_counter")]
+                 "full_du_norm", "ws", "ctrl", "done_counter", "Cpk")]
 
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 SIGNATURES = {
     "dilqr_version": ([], _i),
     "dilqr_model_num_params": ([_i], _i),
+    "dilqr_model_num_ctrl": ([_i], _i),
     "dilqr_dynamics_f32": ([_i, _i, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_linear_dyn_f32": ([_i, _i, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_rollout_f32": ([_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
@@ -54,8 +55,11 @@ SIGNATURES = {
     "dilqr_lqr_adjoint_f32": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _i, _vp, _vp, _vp,
                                _vp, _vp, _vp, _vp], _i),
     "dilqr_implicit_ws_floats": ([_i], _i),
-    "dilqr_mpc_begin_f32": ([_i, _i, _i, _vp, _vp, MpcState, _vp], _i),
+    "dilqr_mpc_packed_cost_floats": ([_i, _i], _i),
+    "dilqr_mpc_begin_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, MpcState, _vp], _i),
     "dilqr_mpc_iterate_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
+    "dilqr_mpc_step_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, MpcState, _vp], _i),
+    "dilqr_mpc_stop_rule_f32": ([_i, _i, _i, _f, _i, MpcState, _vp], _i),
     "dilqr_mpc_gather_best_f32": ([_i, _i, _i, _i, MpcState, _vp, _vp, _vp], _i),
     "dilqr_implicit_backward_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _vp, _vp, _vp,
                                      _vp, _vp], _i),

@@ -152,12 +152,16 @@ class MPCSolve:
         self.ws = torch.empty(T * B * ilqr_ws_floats(n, m), device=dev)
         self.ctrl = torch.zeros(N.CTRL_INTS, dtype=torch.int32, device=dev)
         self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
-        self.state = N.MpcState(*[t.data_ptr() for t in (
+        # packed symmetric-cost copy for the thread-per-problem fused kernels (d <= 8)
+        pk = N.lib().dilqr_mpc_packed_cost_floats(n, m)
+        self.Cpk = torch.empty(T * B * pk, device=dev) if n + m <= 8 else None
+        self.state = N.MpcState(*[t.data_ptr() if t is not None else None for t in (
             self.Xs, self.Us, self.slot, self.best_cost, self.best_du, self.improved, self.cost, self.alpha,
-            self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter)])
+            self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter, self.Cpk)])
 
-    def begin(self, model_id, theta, x_init, u_init=None):
-        """x = get_traj(u_init or 0) into slot 0; reset slots and the control block."""
+    def begin(self, model_id, theta, x_init, u_init=None, C=None, c=None):
+        """x = get_traj(u_init or 0) into slot 0; reset slots and the control
+        block; with the solve's cost (C, c), build its packed copy."""
         if u_init is None:
             self.Us[0].zero_()
         else:
@@ -165,8 +169,8 @@ class MPCSolve:
             if u0.ndimension() == 2:
                 u0 = u0.unsqueeze(1).expand(self.T, self.B, self.m)
             self.Us[0].copy_(u0)
-        N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), self.state,
-               N.stream(x_init.device))
+        N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), N.ptr(C), N.ptr(c),
+               self.state, N.stream(x_init.device))
 
     def iterate(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, first, best_cost_eps, eps,
                 not_improved_lim):
@@ -201,7 +205,7 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     m = C.shape[-1] - n
     x_init, C, c = _f32(x_init), _f32(C), _f32(c)
     sv = MPCSolve(T, B, n, m, x_init.device)
-    sv.begin(model_id, theta, x_init, u_init)
+    sv.begin(model_id, theta, x_init, u_init, C, c)
     bounds, keep = N.make_bounds(u_lower, u_upper)
     for i in range(lqr_iter):
         sv.iterate(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i == 0,

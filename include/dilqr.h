@@ -66,6 +66,7 @@ int dilqr_version(void);
 
 /* Number of parameters theta of a model (4 for cartpole), or -1. */
 int dilqr_model_num_params(int model);
+int dilqr_model_num_ctrl(int model);
 
 /* x' = f(x, u; theta) for N independent rows.  Replaces the models' forward():
    cartpole.py:64-97, pendulum.py:60-95, rocket.py:82-164.
@@ -133,7 +134,8 @@ typedef struct dilqr_mpc_ctrl {
   int n_not_improved;    /* mpc_explicit.py:264, 279                     */
   int any_improved;      /* scratch for the current iteration            */
   unsigned max_du_bits;  /* float bits of max(full_du_norm) this iter    */
-  int pad[3];
+  int cost_packed;       /* 1: the iterations read the packed cost copy  */
+  int pad[2];
 } dilqr_mpc_ctrl;
 
 /* One fused iLQR iteration for a model (not LINDX): linearise on the fly,
@@ -196,28 +198,42 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
    problem's current and best one.  The line search's two candidates roll out
    into the two free slots, so accepting a step size or taking an iterate as
    the new best (mpc_explicit.py:277-283) moves no data.
-   ws: T*B*ceil4(m*n+m+1) floats.  done_counter: one uint (zeroed by begin). */
+   ws: T*B*ceil4(m*n+m+1) floats.  done_counter: one uint (zeroed by begin).
+   Cpk (nullable): T*B*dilqr_mpc_packed_cost_floats(n,m) floats for the solve's
+   packed copy of a symmetric cost (upper triangle of C_t,b, then c_t,b). */
 typedef struct dilqr_mpc_state {
   float* Xs; float* Us; unsigned char* slot; float* best_cost; float* best_du;
   int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;
-  float* ws; dilqr_mpc_ctrl* ctrl; unsigned* done_counter;
+  float* ws; dilqr_mpc_ctrl* ctrl; unsigned* done_counter; float* Cpk;
 } dilqr_mpc_state;
 
 /* Start a solve: x = get_traj(u) from the controls the caller placed in Us
-   slot 0 (zeros or u_init), slots/ctrl reset (mpc_explicit.py:228-249). */
+   slot 0 (zeros or u_init), slots/ctrl reset (mpc_explicit.py:228-249).  With
+   C, c and st.Cpk given (thread-per-problem models), also builds the packed
+   cost copy: when every C_t,b is bitwise symmetric the iterations read 28 (d=6)
+   instead of 42 floats of cost per step, with identical arithmetic; otherwise
+   they read C, c.  The cost passed to the iterations must be the same C, c. */
+int dilqr_mpc_packed_cost_floats(int n, int m);
 int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init,
-                        dilqr_mpc_state st, void* stream);
+                        const float* C, const float* c, dilqr_mpc_state st, void* stream);
 
 /* One MPC iteration (mpc_explicit.py:246-299): the fused linearise + Riccati
    (+pnqp) + line-search kernel on each problem's current slot, best-iterate
    slot update, then the quirk full_du_norm, best_du and the batch-global stop
    rule (max du < eps or n_not_improved > lim) on device.  No-op once stopped.
-   first != 0 for iteration 0. */
+   first != 0 for iteration 0.  = dilqr_mpc_step_f32 + dilqr_mpc_stop_rule_f32. */
 int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const float* x_init,
                           const float* C, const float* c, dilqr_bounds bounds,
                           float linesearch_decay, int max_linesearch_iter, int first,
                           float best_cost_eps, float eps, int not_improved_lim,
                           dilqr_mpc_state st, void* stream);
+/* its two launches, separately (profiling) */
+int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float* x_init,
+                       const float* C, const float* c, dilqr_bounds bounds,
+                       float linesearch_decay, int max_linesearch_iter, int first,
+                       float best_cost_eps, dilqr_mpc_state st, void* stream);
+int dilqr_mpc_stop_rule_f32(int T, int m, int B, float eps, int not_improved_lim,
+                            dilqr_mpc_state st, void* stream);
 
 /* Materialise each problem's best trajectory into x_out [T,B,n], u_out [T,B,m]. */
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out,
