@@ -396,16 +396,67 @@ __global__ void __launch_bounds__(kBlock) k_quirk_norm(int TM, int B, const floa
 // Latency: at B=65536 there is one wave per SIMD, so every loop software-
 // pipelines its HBM loads one step ahead in registers (the step t-1 / t+1
 // record is in flight while step t computes).
+// Private workspaces are component-major ("SoA"): element j of record (t,b) is
+// at [(t*K + j)*B + b], so a wave's 64 lanes touch 64 consecutive words per
+// access (one fully used 256-B run) instead of 64 records K words apart.  For
+// stores this doubles the rate (tools/microbench/store_patterns.hip: 112-B
+// records per lane 3.3 TB/s, coalesced 6.6 TB/s); loads lose little either way.
+// The MPC trajectory slots of the thread-per-problem models use it too
+// ([slot][T][n][B]); the caller's tensors keep the reference layout ("AoS").
+template <int K>
+DEV void ld_soa(float (&r)[K], const float* __restrict__ p, size_t t, int B, int b) {
+#pragma unroll
+  for (int i = 0; i < K; ++i) r[i] = p[(t * K + i) * B + b];
+}
+template <int K>
+DEV void st_soa(float* __restrict__ p, const float (&r)[K], size_t t, int B, int b) {
+#pragma unroll
+  for (int i = 0; i < K; ++i) p[(t * K + i) * B + b] = r[i];
+}
+// records of K floats (K % 4 == 0) as float4 columns: [(t*K/4 + j)*B + b]
+template <int K>
+DEV void ld_soa4(float (&r)[K], const float* __restrict__ p, size_t t, int B, int b) {
+  static_assert(K % 4 == 0, "");
+  const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int j = 0; j < K / 4; ++j) {
+    float4 v = q[(t * (K / 4) + j) * B + b];
+    r[4 * j] = v.x; r[4 * j + 1] = v.y; r[4 * j + 2] = v.z; r[4 * j + 3] = v.w;
+  }
+}
+template <int K>
+DEV void st_soa4(float* __restrict__ p, const float (&r)[K], size_t t, int B, int b) {
+  static_assert(K % 4 == 0, "");
+  float4* q = reinterpret_cast<float4*>(p);
+#pragma unroll
+  for (int j = 0; j < K / 4; ++j) q[(t * (K / 4) + j) * B + b] = make_float4(r[4 * j], r[4 * j + 1], r[4 * j + 2], r[4 * j + 3]);
+}
+
+// trajectories: the caller's [T,B,K] (SOA=false) or the slots' [T,K,B]
+template <bool SOA, int K>
+DEV void ld_traj(float (&r)[K], const float* __restrict__ p, size_t t, int B, int b) {
+  if constexpr (SOA) ld_soa<K>(r, p, t, B, b);
+  else ld(r, p + (t * B + b) * K);
+}
+template <bool SOA, int K>
+DEV void st_traj(float* __restrict__ p, const float (&r)[K], size_t t, int B, int b) {
+  if constexpr (SOA) st_soa<K>(p, r, t, B, b);
+  else st(p + (t * B + b) * K, r);
+}
+
 // Where the fused kernels read the stage cost from: the caller's C [T,B,d,d] and
 // c [T,B,d], or the solve's packed copy (symmetric C: upper triangle row-major,
-// then c, padded to a multiple of 4 floats per (t,b); dilqr_mpc_begin_f32 builds
-// it once per solve when every C_t,b is bitwise symmetric).  Both fill the same
-// full registers, so the arithmetic is identical.
+// then c, padded to a multiple of 4 floats per (t,b), float4-column layout),
+// written by the solve's iteration 0.  Both fill the same full registers, so
+// the arithmetic is identical.
 template <int d>
 struct CostFull {
   const float* __restrict__ C;
   const float* __restrict__ c;
-  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t tb) const { ld2(Cr, C + tb * d * d); ld(cr, c + tb * d); }
+  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t, int B, int b) const {
+    const size_t tb = t * B + b;
+    ld2(Cr, C + tb * d * d); ld(cr, c + tb * d);
+  }
 };
 
 template <int d>
@@ -414,10 +465,10 @@ constexpr int packed_cost_floats() { return ((d * (d + 1) / 2 + d) + 3) / 4 * 4;
 template <int d>
 struct CostPacked {
   const float* __restrict__ P;
-  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t tb) const {
+  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t, int B, int b) const {
     constexpr int PK = packed_cost_floats<d>();
     float buf[PK];
-    ld(buf, P + tb * PK);
+    ld_soa4<PK>(buf, P, t, B, b);
     int k = 0;
 #pragma unroll
     for (int i = 0; i < d; ++i)
@@ -428,31 +479,33 @@ struct CostPacked {
   }
 };
 
-template <int n, int m>
+template <int n, int m, bool SOA>
 struct SweepIn {
   static constexpr int d = n + m;
   float C[d][d], c[d], x[n], u[m];
   template <class CostT>
-  DEV void load(const CostT& cs, const float* __restrict__ xp, const float* __restrict__ up, size_t tb) {
-    cs.load(C, c, tb); ld(x, xp + tb * n); ld(u, up + tb * m);
+  DEV void load(const CostT& cs, const float* __restrict__ xp, const float* __restrict__ up, int t, int B, int b) {
+    cs.load(C, c, t, B, b); ld_traj<SOA>(x, xp, t, B, b); ld_traj<SOA>(u, up, t, B, b);
   }
 };
 
-template <int n, int m, int GREC>
+template <int n, int m, int GREC, bool SOA>
 struct FwdIn {
   static constexpr int d = n + m;
   float g[GREC], u[m], C[d][d], c[d], xnext[n];
   template <class CostT>
   DEV void load(const float* __restrict__ grec, const float* __restrict__ up, const CostT& cs,
-                const float* __restrict__ xp, size_t tb, size_t tb1) {
-    ld(g, grec + tb * GREC); ld(u, up + tb * m); cs.load(C, c, tb);
-    ld(xnext, xp + tb1 * n);
+                const float* __restrict__ xp, int t, int t1, int B, int b) {
+    ld_soa4<GREC>(g, grec, t, B, b); ld_traj<SOA>(u, up, t, B, b); cs.load(C, c, t, B, b);
+    ld_traj<SOA>(xnext, xp, t1, B, b);
   }
 };
 
-template <class Model, int MODE, class CostT>
+// x, u (current trajectory) and the candidate outputs in layout SOA; the gain
+// records in ws and the packed cost are always float4-column.
+template <class Model, int MODE, bool SOA, class CostT>
 DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
-                     const float* __restrict__ x,
+                     float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
                      float* __restrict__ ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
                      float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
@@ -463,16 +516,34 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
   {
     RiccatiState<n, m> rs;
     rs.init();
-    SweepIn<n, m> cur, nxt;
-    cur.load(cs, x, u, (size_t)(T - 1) * B + b);
+    bool sym = true;
+    SweepIn<n, m, SOA> cur, nxt;
+    cur.load(cs, x, u, T - 1, B, b);
     for (int t = T - 1; t >= 0; --t) {
       size_t tb = (size_t)t * B + b;
-      nxt.load(cs, x, u, (size_t)(t > 0 ? t - 1 : 0) * B + b);        // prefetch step t-1
+      nxt.load(cs, x, u, t > 0 ? t - 1 : 0, B, b);                     // prefetch step t-1
       float tau[d], Ctau[d], cb[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
 #pragma unroll
       for (int a = 0; a < m; ++a) tau[n + a] = cur.u[a];
+      if (pack_out) {                                   // first iteration: build the packed copy
+        constexpr int PK = packed_cost_floats<d>();
+        float buf[PK];
+        int kk = 0;
+#pragma unroll
+        for (int i = 0; i < d; ++i)
+#pragma unroll
+          for (int j = i; j < d; ++j) {
+            sym &= __float_as_uint(cur.C[i][j]) == __float_as_uint(cur.C[j][i]);
+            buf[kk++] = cur.C[i][j];
+          }
+#pragma unroll
+        for (int i = 0; i < d; ++i) buf[kk++] = cur.c[i];
+#pragma unroll
+        for (; kk < PK; ++kk) buf[kk] = 0.f;
+        st_soa4<PK>(pack_out, buf, t, B, b);
+      }
       float obj = quad_cost(cur.C, cur.c, tau, Ctau);
 #pragma unroll
       for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + cur.c[i];
@@ -506,9 +577,10 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       g[m * n + m] = obj;
 #pragma unroll
       for (int i = m * n + m + 1; i < GREC; ++i) g[i] = 0.f;
-      st(ws + tb * GREC, g);
+      st_soa4<GREC>(ws, g, t, B, b);
       cur = nxt;
     }
+    if (sym_out) sym_out[b] = sym ? 1 : 0;
   }
   // ---------------- forward: the line search (lqr_step_explicit.py:166-263).
   // Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
@@ -525,17 +597,17 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     ld(xA, x_init + (size_t)b * n);
 #pragma unroll
     for (int i = 0; i < n; ++i) { dA[i] = 0.f; xB[i] = xA[i]; dB[i] = 0.f; }
-    st(xa_out + (size_t)b * n, xA);
-    if (twoB) st(xb_out + (size_t)b * n, xB);
+    st_traj<SOA>(xa_out, xA, 0, B, b);
+    if (twoB) st_traj<SOA>(xb_out, xB, 0, B, b);
     float cA = 0.f, cB = 0.f, oldc = 0.f;
-    FwdIn<n, m, GREC> cur, nxt;
-    cur.load(ws, u, cs, x, (size_t)b, (size_t)(T > 1 ? 1 : 0) * B + b);
+    FwdIn<n, m, GREC, SOA> cur, nxt;
+    cur.load(ws, u, cs, x, 0, T > 1 ? 1 : 0, B, b);
     for (int t = 0; t < T; ++t) {
       const size_t tb = (size_t)t * B + b;
       {
         int t1 = t + 1 < T ? t + 1 : t;                 // prefetch step t+1
         int t2 = t + 2 < T ? t + 2 : t1;
-        nxt.load(ws, u, cs, x, (size_t)t1 * B + b, (size_t)t2 * B + b);
+        nxt.load(ws, u, cs, x, t1, t2, B, b);
       }
       float nuA[m], nuB[m];
 #pragma unroll
@@ -555,8 +627,8 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
         }
       }
       oldc += cur.g[m * n + m];
-      st(ua_out + tb * m, nuA);
-      if (twoB) st(ub_out + tb * m, nuB);
+      st_traj<SOA>(ua_out, nuA, t, B, b);
+      if (twoB) st_traj<SOA>(ub_out, nuB, t, B, b);
       if (p == 0) {
 #pragma unroll
         for (int a = 0; a < m; ++a) {
@@ -585,7 +657,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
           dA[i] = xnext[i] - cur.xnext[i];
           xA[i] = xnext[i];
         }
-        st(xa_out + (tb + B) * n, xA);
+        st_traj<SOA>(xa_out, xA, t + 1, B, b);
         if (twoB) {
           md.forward(xB, nuB, xnext);
 #pragma unroll
@@ -593,7 +665,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
             dB[i] = xnext[i] - cur.xnext[i];
             xB[i] = xnext[i];
           }
-          st(xb_out + (tb + B) * n, xB);
+          st_traj<SOA>(xb_out, xB, t + 1, B, b);
         }
       }
       cur = nxt;
@@ -628,7 +700,9 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
   // over (x_out, u_out) when it wins
   float* xb = ws + (size_t)T * B * GREC;
   float* ub = xb + (size_t)T * B * n;
-  const int win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, CostFull<n + m>{C, c}, x, u, bd, decay, max_ls, ws,
+  const int win = ilqr_problem<Model, MODE, false>(T, B, b, md, x_init, CostFull<n + m>{C, c}, nullptr, nullptr, x, u,
+                                                   bd, decay,
+                                            max_ls, ws,
                                             x_out, u_out, xb, ub, du_sq, cost, alpha);
   if (win) {
     for (int t = 0; t < T; ++t) {
@@ -680,13 +754,18 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   free_slots(cur, best, sa, sb);
   float cost, alpha;
   int win;
-  if (S.ctrl->cost_packed)       // uniform: set once per solve by dilqr_mpc_begin_f32
-    win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk}, S.Xs + cur * TBn,
-                                    S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm,
-                                    S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost, alpha);
+  // the solve's packed symmetric cost: built by iteration 0's sweep (which reads
+  // C, c), used from iteration 1 on by every problem whose C_t are all bitwise
+  // symmetric (per-lane flag; a wave normally takes one side of the branch)
+  const CostFull<n + m> full{C, c};
+  if (!first && S.Cpk && S.cost_sym[b])
+    win = ilqr_problem<Model, MODE, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk}, nullptr, nullptr,
+                                    S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn,
+                                    S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost, alpha);
   else
-    win = ilqr_problem<Model, MODE>(T, B, b, md, x_init, CostFull<n + m>{C, c}, S.Xs + cur * TBn, S.Us + cur * TBm,
-                                    bd, decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
+    win = ilqr_problem<Model, MODE, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
+                                    first && S.Cpk ? S.cost_sym : nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd,
+                                    decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
                                     S.Us + sb * TBm, S.du_sq, cost, alpha);
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
@@ -782,9 +861,9 @@ __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float e
     const size_t base = (size_t)blockIdx.x * blockDim.x * TM;
     const size_t total = (size_t)B * TM;
     const int span = blockDim.x * TM;
-    // 8 independent loads in flight per thread before the first LDS store
-    // (a load->store loop would serialise one HBM latency per element)
-    constexpr int U = 8;
+    // up to 32 independent loads in flight per thread before the first LDS
+    // store (a load->store loop would serialise one HBM latency per element)
+    constexpr int U = 32;
     for (int i0 = threadIdx.x; i0 < span; i0 += blockDim.x * U) {
       float v[U];
 #pragma unroll
@@ -813,7 +892,8 @@ __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float e
     if (imp) S.best_du[r] = fdn;
     any = imp == 2;
   }
-  // wave reduction (64 lanes), then across the block's 4 waves, one atomic per block
+  // wave reduction (64 lanes), then across the block's waves -> this block's
+  // partial (plain stores, no contended atomics)
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     unsigned o = __shfl_xor(mx, off, 64);
@@ -823,86 +903,97 @@ __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float e
   int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { red_max[w] = mx; red_any[w] = any; }
   __syncthreads();
+  // sync area: [0,8) arrivals per XCD, [8] XCD arrivals, [16, 16+G) block max
+  // bits, [16+G, 16+2G) block any (G = gridDim.x).  Hierarchical fan-in:
+  // workgroups land round-robin on the 8 XCDs, so blockIdx.x % 8 counters take
+  // ~G/8 arrivals each and the last arriver of each XCD one more on [8].
+  unsigned* sync = S.done_counter;
+  const unsigned G = gridDim.x;
   if (threadIdx.x == 0) {
     unsigned bm = red_max[0];
     int ba = red_any[0];
     for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { bm = red_max[i] > bm ? red_max[i] : bm; ba |= red_any[i]; }
-    atomicMax(&S.ctrl->max_du_bits, bm);
-    if (ba) atomicOr(&S.ctrl->any_improved, 1);
+    sync[16 + blockIdx.x] = bm;
+    sync[16 + G + blockIdx.x] = (unsigned)ba;
+    const unsigned x = blockIdx.x & 7u;
+    const unsigned in_x = (G - x + 7u) / 8u;                  // blocks of this XCD
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    unsigned prev = atomicAdd(S.done_counter, 1u);
-    last = (prev == gridDim.x - 1);
+    int lst = 0;
+    if (atomicAdd(&sync[x], 1u) == in_x - 1u) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const unsigned nx = G < 8u ? G : 8u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      lst = atomicAdd(&sync[8], 1u) == nx - 1u;
+    }
+    last = lst;
   }
   __syncthreads();
-  if (last && threadIdx.x == 0) {
+  if (last) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    dilqr_mpc_ctrl* ctl = S.ctrl;
-    int anyi = __hip_atomic_load(&ctl->any_improved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned mxb = __hip_atomic_load(&ctl->max_du_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ctl->iter += 1;
-    ctl->n_not_improved += 1;
-    if (anyi) ctl->n_not_improved = 0;
-    if (__uint_as_float(mxb) < eps || ctl->n_not_improved > not_improved_lim) ctl->stopped = 1;
-    __hip_atomic_store(&ctl->any_improved, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&ctl->max_du_bits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(S.done_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned bm = 0u;
+    int ba = 0;
+    for (unsigned i = threadIdx.x; i < G; i += blockDim.x) {
+      unsigned v = __hip_atomic_load(&sync[16 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bm = v > bm ? v : bm;
+      ba |= (int)__hip_atomic_load(&sync[16 + G + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      unsigned o = __shfl_xor(bm, off, 64);
+      bm = o > bm ? o : bm;
+      ba |= __shfl_xor(ba, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) { red_max[w] = bm; red_any[w] = ba; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { bm = red_max[i] > bm ? red_max[i] : bm; ba |= red_any[i]; }
+      bm = red_max[0] > bm ? red_max[0] : bm;
+      ba |= red_any[0];
+      dilqr_mpc_ctrl* ctl = S.ctrl;
+      ctl->iter += 1;
+      ctl->n_not_improved += 1;
+      if (ba) ctl->n_not_improved = 0;
+      if (__uint_as_float(bm) < eps || ctl->n_not_improved > not_improved_lim) ctl->stopped = 1;
+      ctl->max_du_bits = bm;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) __hip_atomic_store(&sync[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
+
+// slot layout: component-major for the thread-per-problem models, the
+// caller's [T,B,k] for the 16-lanes-per-problem ones
+template <class Model>
+constexpr bool soa_slots() { return Model::N + Model::M <= 8; }
+constexpr bool soa_slots_nm(int n, int m) { return n + m <= 8; }
 
 // rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl.
 template <class Model>
 __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float* __restrict__ theta,
-                                                      const float* __restrict__ x_init, int pack, MpcState S) {
+                                                      const float* __restrict__ x_init, MpcState S) {
   constexpr int n = Model::N, m = Model::M;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b == 0) {
     dilqr_mpc_ctrl z = {};
-    z.cost_packed = pack ? 1 : 0;      // cleared by k_pack_cost on any asymmetric C
     *S.ctrl = z;
-    *S.done_counter = 0u;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) S.done_counter[i] = 0u;
   }
   if (b >= B) return;
   Model md; md.load(theta);
   S.slot[b] = 0; S.slot[B + b] = 0;
+  constexpr bool SOA = soa_slots<Model>();
   float xt[n];
   ld(xt, x_init + (size_t)b * n);
-  st(S.Xs + (size_t)b * n, xt);
+  st_traj<SOA>(S.Xs, xt, 0, B, b);
   for (int t = 0; t < T - 1; ++t) {
     float ut[m], xn[n];
-    ld(ut, S.Us + ((size_t)t * B + b) * m);
+    ld_traj<SOA>(ut, S.Us, t, B, b);
     md.forward(xt, ut, xn);
 #pragma unroll
     for (int i = 0; i < n; ++i) xt[i] = xn[i];
-    st(S.Xs + ((size_t)(t + 1) * B + b) * n, xt);
+    st_traj<SOA>(S.Xs, xt, t + 1, B, b);
   }
-}
-
-// the solve's packed cost copy (CostPacked) + the bitwise symmetry check
-template <int d>
-__global__ void __launch_bounds__(256) k_pack_cost(long long TB, const float* __restrict__ C,
-                                                   const float* __restrict__ c, float* __restrict__ P,
-                                                   dilqr_mpc_ctrl* __restrict__ ctrl) {
-  constexpr int PK = packed_cost_floats<d>();
-  const long long tb = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tb >= TB) return;
-  float Cr[d][d], cr[d], buf[PK];
-  ld2(Cr, C + tb * d * d);
-  ld(cr, c + tb * d);
-  bool sym = true;
-  int k = 0;
-#pragma unroll
-  for (int i = 0; i < d; ++i)
-#pragma unroll
-    for (int j = i; j < d; ++j) {
-      sym &= __float_as_uint(Cr[i][j]) == __float_as_uint(Cr[j][i]);
-      buf[k++] = Cr[i][j];
-    }
-#pragma unroll
-  for (int i = 0; i < d; ++i) buf[k++] = cr[i];
-#pragma unroll
-  for (; k < PK; ++k) buf[k] = 0.f;
-  st(P + tb * PK, buf);
-  if (__any(!sym) && (threadIdx.x & 63) == 0) atomicExch(&ctrl->cost_packed, 0);
 }
 
 template <int n, int m>
@@ -911,12 +1002,13 @@ __global__ void __launch_bounds__(kBlock) k_mpc_gather(int T, int B, MpcState S,
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   int best = S.slot[B + b];
+  constexpr bool SOA = soa_slots_nm(n, m);
   const float* X = S.Xs + (size_t)best * T * B * n;
   const float* U = S.Us + (size_t)best * T * B * m;
   for (int t = 0; t < T; ++t) {
     size_t tb = (size_t)t * B + b;
     float xt[n], ut[m];
-    ld(xt, X + tb * n); ld(ut, U + tb * m);
+    ld_traj<SOA>(xt, X, t, B, b); ld_traj<SOA>(ut, U, t, B, b);
     st(x_out + tb * n, xt); st(u_out + tb * m, ut);
   }
 }
@@ -1799,7 +1891,7 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta, con
 static bool bad_state(const dilqr_mpc_state& st) {
   return !st.Xs || !st.Us || !st.slot || !st.best_cost || !st.best_du || !st.improved || !st.cost || !st.alpha ||
          !st.du_sq || !st.full_du_norm || !st.ws || !st.ctrl || !st.done_counter || !al16(st.Xs) || !al16(st.Us) ||
-         !al16(st.ws);
+         !al16(st.ws) || (st.Cpk && (!st.cost_sym || !al16(st.Cpk)));
 }
 
 int dilqr_mpc_packed_cost_floats(int n, int m) {
@@ -1807,21 +1899,10 @@ int dilqr_mpc_packed_cost_floats(int n, int m) {
   return d < 1 ? -1 : ((d * (d + 1) / 2 + d) + 3) / 4 * 4;
 }
 
-int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
-                        const float* c, dilqr_mpc_state st, void* stream) {
+int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init, dilqr_mpc_state st,
+                        void* stream) {
   if (T < 1 || B < 0 || !theta || !x_init || !al16(x_init) || bad_state(st)) return DILQR_E_ARG;
-  if ((C && !al16(C)) || (c && !al16(c)) || !al16(st.Cpk)) return DILQR_E_ARG;
-  // the packed copy serves the thread-per-problem fused kernels
-  const int pack = (C && c && st.Cpk && B > 0 && model != DILQR_MODEL_ROCKET) ? 1 : 0;
-  MODEL_SWITCH(model, (k_mpc_begin<MD><<<grid_for(B > 0 ? B : 1), kBlock, 0, S(stream)>>>(T, B, theta, x_init, pack,
-                                                                                          st)));
-  if (pack) {
-    int e = launched();
-    if (e) return e;
-    const long long TB = (long long)T * B;
-    MODEL_SWITCH_TPP(model, (k_pack_cost<MD::N + MD::M><<<(int)((TB + 255) / 256), 256, 0, S(stream)>>>(
-                                 TB, C, c, st.Cpk, st.ctrl)));
-  }
+  MODEL_SWITCH(model, (k_mpc_begin<MD><<<grid_for(B > 0 ? B : 1), kBlock, 0, S(stream)>>>(T, B, theta, x_init, st)));
   return launched();
 }
 

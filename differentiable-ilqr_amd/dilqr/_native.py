@@ -32,7 +32,7 @@ class MpcState(ctypes.Structure):
     """dilqr_mpc_state: device pointers of one MPC solve (include/dilqr.h)."""
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("Xs", "Us", "slot", "best_cost", "best_du", "improved", "cost", "alpha", "du_sq",
-                 "full_du_norm", "ws", "ctrl", "done_counter", "Cpk")]
+                 "full_du_norm", "ws", "ctrl", "done_counter", "Cpk", "cost_sym")]
 
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 SIGNATURES = {
@@ -56,7 +56,7 @@ SIGNATURES = {
                                _vp, _vp, _vp, _vp], _i),
     "dilqr_implicit_ws_floats": ([_i], _i),
     "dilqr_mpc_packed_cost_floats": ([_i, _i], _i),
-    "dilqr_mpc_begin_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, MpcState, _vp], _i),
+    "dilqr_mpc_begin_f32": ([_i, _i, _i, _vp, _vp, MpcState, _vp], _i),
     "dilqr_mpc_iterate_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
     "dilqr_mpc_step_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, MpcState, _vp], _i),
     "dilqr_mpc_stop_rule_f32": ([_i, _i, _i, _f, _i, MpcState, _vp], _i),

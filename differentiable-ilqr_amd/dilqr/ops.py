@@ -139,8 +139,11 @@ class MPCSolve:
     def __init__(self, T, B, n, m, device):
         dev = device
         self.T, self.B, self.n, self.m = T, B, n, m
-        self.Xs = torch.empty(4, T, B, n, device=dev)
-        self.Us = torch.zeros(4, T, B, m, device=dev)
+        # slots are component-major [4,T,n,B] for the thread-per-problem models
+        # (coalesced per-lane access), the caller's [4,T,B,n] for rocket
+        self.soa = n + m <= 8
+        self.Xs = torch.empty((4, T, n, B) if self.soa else (4, T, B, n), device=dev)
+        self.Us = torch.zeros((4, T, m, B) if self.soa else (4, T, B, m), device=dev)
         self.slot = torch.zeros(2, B, dtype=torch.uint8, device=dev)
         self.best_cost = torch.empty(B, device=dev)
         self.best_du = torch.empty(B, device=dev)
@@ -151,26 +154,27 @@ class MPCSolve:
         self.full_du_norm = torch.empty(B, device=dev)
         self.ws = torch.empty(T * B * ilqr_ws_floats(n, m), device=dev)
         self.ctrl = torch.zeros(N.CTRL_INTS, dtype=torch.int32, device=dev)
-        self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
+        # stop-rule sync area: 16 counters + per-block partials (<= ceil(B/64) blocks)
+        self.counter = torch.zeros(16 + 2 * ((B + 63) // 64), dtype=torch.int32, device=dev)
         # packed symmetric-cost copy for the thread-per-problem fused kernels (d <= 8)
         pk = N.lib().dilqr_mpc_packed_cost_floats(n, m)
         self.Cpk = torch.empty(T * B * pk, device=dev) if n + m <= 8 else None
+        self.cost_sym = torch.zeros(B, dtype=torch.uint8, device=dev) if self.Cpk is not None else None
         self.state = N.MpcState(*[t.data_ptr() if t is not None else None for t in (
             self.Xs, self.Us, self.slot, self.best_cost, self.best_du, self.improved, self.cost, self.alpha,
-            self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter, self.Cpk)])
+            self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter, self.Cpk, self.cost_sym)])
 
-    def begin(self, model_id, theta, x_init, u_init=None, C=None, c=None):
-        """x = get_traj(u_init or 0) into slot 0; reset slots and the control
-        block; with the solve's cost (C, c), build its packed copy."""
+    def begin(self, model_id, theta, x_init, u_init=None):
+        """x = get_traj(u_init or 0) into slot 0; reset slots and the control block."""
         if u_init is None:
             self.Us[0].zero_()
         else:
             u0 = u_init.to(device=self.Us.device, dtype=torch.float32)
             if u0.ndimension() == 2:
                 u0 = u0.unsqueeze(1).expand(self.T, self.B, self.m)
-            self.Us[0].copy_(u0)
-        N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), N.ptr(C), N.ptr(c),
-               self.state, N.stream(x_init.device))
+            self.Us[0].copy_(u0.permute(0, 2, 1) if self.soa else u0)
+        N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), self.state,
+               N.stream(x_init.device))
 
     def iterate(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, first, best_cost_eps, eps,
                 not_improved_lim):
@@ -205,7 +209,7 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     m = C.shape[-1] - n
     x_init, C, c = _f32(x_init), _f32(C), _f32(c)
     sv = MPCSolve(T, B, n, m, x_init.device)
-    sv.begin(model_id, theta, x_init, u_init, C, c)
+    sv.begin(model_id, theta, x_init, u_init)
     bounds, keep = N.make_bounds(u_lower, u_upper)
     for i in range(lqr_iter):
         sv.iterate(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i == 0,

@@ -134,8 +134,7 @@ typedef struct dilqr_mpc_ctrl {
   int n_not_improved;    /* mpc_explicit.py:264, 279                     */
   int any_improved;      /* scratch for the current iteration            */
   unsigned max_du_bits;  /* float bits of max(full_du_norm) this iter    */
-  int cost_packed;       /* 1: the iterations read the packed cost copy  */
-  int pad[2];
+  int pad[3];
 } dilqr_mpc_ctrl;
 
 /* One fused iLQR iteration for a model (not LINDX): linearise on the fly,
@@ -193,29 +192,33 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
                                 float* dC, float* dc, float* dtheta, void* stream);
 
 /* ---- the device-resident MPC loop with per-problem trajectory slots ------ */
-/* Caller-owned device buffers of one solve.  Xs [4,T,B,n] and Us [4,T,B,m] hold
-   four trajectories per problem; slot [2,B] (uint8) the indices of each
+/* Caller-owned device buffers of one solve.  Xs and Us hold four trajectories
+   per problem, component-major [4,T,n,B] / [4,T,m,B] for the pendulum and
+   cartpole (coalesced per-lane access) and [4,T,B,n] / [4,T,B,m] for rocket; slot [2,B] (uint8) the indices of each
    problem's current and best one.  The line search's two candidates roll out
    into the two free slots, so accepting a step size or taking an iterate as
    the new best (mpc_explicit.py:277-283) moves no data.
-   ws: T*B*ceil4(m*n+m+1) floats.  done_counter: one uint (zeroed by begin).
-   Cpk (nullable): T*B*dilqr_mpc_packed_cost_floats(n,m) floats for the solve's
-   packed copy of a symmetric cost (upper triangle of C_t,b, then c_t,b). */
+   ws: T*B*ceil4(m*n+m+1) floats.  done_counter: the stop rule's sync area of
+   16 + 2*ceil(B/64) uints (its counters are zeroed by begin).
+   Cpk (nullable) + cost_sym [B] (uint8): the solve's packed copy of a
+   symmetric cost, T*B*dilqr_mpc_packed_cost_floats(n,m) floats (upper triangle
+   of C_t,b row-major, then c_t,b, zero-padded to a multiple of 4).  Iteration 0
+   (first != 0) reads C, c and writes the copy and, per problem, whether all its
+   C_t are bitwise symmetric; later iterations of those problems read the copy
+   (28 instead of 42 floats per step at d=6; identical arithmetic).  The cost
+   passed to the iterations of one solve must not change. */
 typedef struct dilqr_mpc_state {
   float* Xs; float* Us; unsigned char* slot; float* best_cost; float* best_du;
   int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;
   float* ws; dilqr_mpc_ctrl* ctrl; unsigned* done_counter; float* Cpk;
+  unsigned char* cost_sym;
 } dilqr_mpc_state;
 
 /* Start a solve: x = get_traj(u) from the controls the caller placed in Us
-   slot 0 (zeros or u_init), slots/ctrl reset (mpc_explicit.py:228-249).  With
-   C, c and st.Cpk given (thread-per-problem models), also builds the packed
-   cost copy: when every C_t,b is bitwise symmetric the iterations read 28 (d=6)
-   instead of 42 floats of cost per step, with identical arithmetic; otherwise
-   they read C, c.  The cost passed to the iterations must be the same C, c. */
+   slot 0 (zeros or u_init), slots/ctrl reset (mpc_explicit.py:228-249). */
 int dilqr_mpc_packed_cost_floats(int n, int m);
 int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init,
-                        const float* C, const float* c, dilqr_mpc_state st, void* stream);
+                        dilqr_mpc_state st, void* stream);
 
 /* One MPC iteration (mpc_explicit.py:246-299): the fused linearise + Riccati
    (+pnqp) + line-search kernel on each problem's current slot, best-iterate
