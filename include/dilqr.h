@@ -202,11 +202,11 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
    16 + 2*ceil(B/64) uints (its counters are zeroed by begin).
    Cpk (nullable) + cost_sym [B] (uint8): the solve's packed copy of a
    symmetric cost, T*B*dilqr_mpc_packed_cost_floats(n,m) floats (upper triangle
-   of C_t,b row-major, then c_t,b, zero-padded to a multiple of 4).  Iteration 0
-   (first != 0) reads C, c and writes the copy and, per problem, whether all its
-   C_t are bitwise symmetric; later iterations of those problems read the copy
-   (28 instead of 42 floats per step at d=6; identical arithmetic).  The cost
-   passed to the iterations of one solve must not change. */
+   of C_t,b row-major, then c_t,b; component-major).  Iteration 0 (first != 0)
+   reads C, c and writes the copy and, per problem, whether all its C_t are
+   bitwise symmetric; later iterations of those problems read the copy (27
+   instead of 42 floats per step at d=6; identical arithmetic).  The cost passed
+   to the iterations of one solve must not change. */
 typedef struct dilqr_mpc_state {
   float* Xs; float* Us; unsigned char* slot; float* best_cost; float* best_du;
   int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;

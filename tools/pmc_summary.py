@@ -35,7 +35,7 @@ def main(pmc_dir, round_tag):
                 agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
     for k, cs in agg.items():
-        out[k] = {c: sum(v) / len(v) for c, v in cs.items()}
+        out[k] = {c: sorted(v)[len(v) // 2] for c, v in cs.items()}   # median launch
         if "FETCH_SIZE" in out[k] and "WRITE_SIZE" in out[k]:
             out[k]["hbm_bytes_per_launch"] = (2 * out[k]["FETCH_SIZE"] + out[k]["WRITE_SIZE"]) * 1024
     os.makedirs(os.path.join(ROOT, "profiles", round_tag), exist_ok=True)
