@@ -87,7 +87,7 @@ def _timed_solves(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, lqr_iter
     def solve():
         sv.begin(model_id, theta, x0)
         for i in range(lqr_iter):
-            sv.iterate(model_id, theta, x0, C, c, bounds, decay, max_ls, i == 0, 1e-4, 0.0, 10 ** 9)
+            sv.iterate(model_id, theta, x0, C, c, bounds, decay, max_ls, i, 1e-4, 0.0, 10 ** 9)
     for _ in range(warmup_solves):
         solve()
     torch.cuda.synchronize()
@@ -258,10 +258,10 @@ def main():
     state = {"i": 0}
 
     def step():
-        first = state["i"] % args.lqr_iter == 0
-        if first:
+        it = state["i"] % args.lqr_iter
+        if it == 0:
             sv.begin(N.MODEL_CARTPOLE, theta, x0)
-        sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, first, 1e-4, 0.0, 10 ** 9)
+        sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, it, 1e-4, 0.0, 10 ** 9)
         state["i"] += 1
 
     if args.kernels_only:
@@ -292,14 +292,14 @@ def main():
     reps = 10
     # (iterations 1..reps of a solve: iteration 0 also builds the packed cost copy)
     sv.begin(N.MODEL_CARTPOLE, theta, x0)
-    sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, True, 1e-4, 0.0, 10 ** 9)
+    sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for r in range(reps):
         ev[r][0].record(stream)
         N.call("dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C), N.ptr(c),
-               bounds, 0.5, 2, 0, 1e-4, sv.state, s)
+               bounds, 0.5, 2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s)
         ev[r][1].record(stream)
-        N.call("dilqr_mpc_stop_rule_f32", T_HORIZON, N_CTRL, B, 0.0, 10 ** 9, sv.state, s)
+        N.call("dilqr_mpc_stop_rule_f32", T_HORIZON, N_CTRL, B, r + 1, sv.state, s)
     torch.cuda.synchronize(dev)
     iter_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     iter_bytes = ITER_BYTES_PER_PROBLEM * B

@@ -752,6 +752,8 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
 using MpcState = dilqr_mpc_state;
 constexpr int kSlots = 4;
 
+DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim);
+
 // the two lowest slot indices not in {cur, best}
 DEV void free_slots(int cur, int best, int& sa, int& sb) {
   int k = 0;
@@ -770,9 +772,11 @@ template <class Model, int MODE>
 __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const float* __restrict__ theta,
                                                         const float* __restrict__ x_init, const float* __restrict__ C,
                                                         const float* __restrict__ c, Bounds bd, float decay, int max_ls,
-                                                        int first, float best_cost_eps, MpcState S) {
+                                                        int iteration, float best_cost_eps, float eps,
+                                                        int not_improved_lim, int G, MpcState S) {
   constexpr int n = Model::N, m = Model::M;
-  if (S.ctrl->stopped) return;
+  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
+  const int first = iteration == 0;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   Model md; md.load(theta);
@@ -838,11 +842,13 @@ template <class Model, int MODE>
 __global__ void __launch_bounds__(64) k_mpc_iterate_group(int T, int B, const float* __restrict__ theta,
                                                           const float* __restrict__ x_init,
                                                           const float* __restrict__ C, const float* __restrict__ c,
-                                                          Bounds bd, float decay, int max_ls, int first,
-                                                          float best_cost_eps, MpcState S) {
+                                                          Bounds bd, float decay, int max_ls, int iteration,
+                                                          float best_cost_eps, float eps, int not_improved_lim, int G,
+                                                          MpcState S) {
   constexpr int n = Model::N, m = Model::M;
   __shared__ GroupLds<n, m> Ls[kGPW];
-  if (S.ctrl->stopped) return;
+  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
+  const int first = iteration == 0;
   const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
   const int b0 = blockIdx.x * kGPW + gp;
   const bool valid = b0 < B;
@@ -868,22 +874,31 @@ __global__ void __launch_bounds__(64) k_mpc_iterate_group(int T, int B, const fl
   }
 }
 
-// full_du_norm (the reference's batch-mixing rows), best_du for the problems
-// that took this iterate, then — in the last workgroup to finish — the stop
-// rule (mpc_explicit.py:264, 279, 297-299).  Cross-workgroup hand-off: every
-// workgroup's contributions are device-scope atomics; a release fence before and
-// an acquire fence after the arrival counter make them visible to the last one.
+// ---------------- the stop rule (mpc_explicit.py:264, 279, 297-299), split so
+// that no launch waits on a grid-wide fan-in:
+//  * k_mpc_norm_rows (after iteration k): full_du_norm with the reference's
+//    batch-mixing rows (the .transpose(1,2).contiguous().view(n_batch,-1) quirk,
+//    lqr_step_explicit.py:245-247), best_du of the problems that took iteration
+//    k, and per-workgroup partials (max row norm, any "improved") into plane
+//    k&1 of the sync area.  Plain stores only.
+//  * mpc_decide, in the prologue of iteration k+1 (every workgroup, redundantly,
+//    identically): reduce the partials of iteration k, apply the stop rule to the
+//    control state S_k -> S_{k+1}; workgroup 0 publishes S_{k+1} in ctrl[(k+1)&1].
+//    The kernel boundary orders everything, so no fences or atomics are needed
+//    (measured: the former last-workgroup fan-in cost 8 of 14 us per iteration).
+// Sync area (uints): [16 + (2*par + 0)*G_MAX + blk] max bits, [16 + (2*par+1)*G_MAX
+// + blk] any, G_MAX = ceil(B/64).
+DEV int sync_gmax(int B) { return (B + 63) / 64; }
+
 template <bool STAGE>
-__global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float eps, int not_improved_lim,
-                                                          MpcState S) {
-  // the block's rows are one contiguous span of TM*256 floats: stage it through
-  // LDS with coalesced loads, then each thread sums its row (stride TM words;
-  // TM odd -> conflict-free, TM even -> at most 2-way)
+__global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iteration, MpcState S) {
+  // the block's rows are one contiguous span of TM*blockDim floats: stage it
+  // through LDS with coalesced loads, then each thread sums its row (stride TM
+  // words; TM odd -> conflict-free, TM even -> at most 2-way)
   extern __shared__ __attribute__((aligned(16))) float sdu[];
   __shared__ unsigned red_max[4];
   __shared__ int red_any[4];
-  __shared__ int last;
-  if (S.ctrl->stopped) return;
+  if (S.ctrl[iteration & 1].stopped) return;          // iteration `iteration` did not run
   int r = blockIdx.x * blockDim.x + threadIdx.x;
   if constexpr (STAGE) {
     const size_t base = (size_t)blockIdx.x * blockDim.x * TM;
@@ -905,8 +920,8 @@ __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float e
         if (i < span) sdu[i] = v[j];
       }
     }
+    __syncthreads();
   }
-  if constexpr (STAGE) __syncthreads();
   unsigned mx = 0u;
   int any = 0;
   if (r < B) {
@@ -920,73 +935,54 @@ __global__ void __launch_bounds__(256) k_mpc_norm_control(int TM, int B, float e
     if (imp) S.best_du[r] = fdn;
     any = imp == 2;
   }
-  // wave reduction (64 lanes), then across the block's waves -> this block's
-  // partial (plain stores, no contended atomics)
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     unsigned o = __shfl_xor(mx, off, 64);
     mx = o > mx ? o : mx;
     any |= __shfl_xor(any, off, 64);
   }
-  int w = threadIdx.x >> 6;
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { red_max[w] = mx; red_any[w] = any; }
   __syncthreads();
-  // sync area: [0,8) arrivals per XCD, [8] XCD arrivals, [16, 16+G) block max
-  // bits, [16+G, 16+2G) block any (G = gridDim.x).  Hierarchical fan-in:
-  // workgroups land round-robin on the 8 XCDs, so blockIdx.x % 8 counters take
-  // ~G/8 arrivals each and the last arriver of each XCD one more on [8].
-  unsigned* sync = S.done_counter;
-  const unsigned G = gridDim.x;
   if (threadIdx.x == 0) {
-    unsigned bm = red_max[0];
-    int ba = red_any[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { bm = red_max[i] > bm ? red_max[i] : bm; ba |= red_any[i]; }
-    sync[16 + blockIdx.x] = bm;
-    sync[16 + G + blockIdx.x] = (unsigned)ba;
-    const unsigned x = blockIdx.x & 7u;
-    const unsigned in_x = (G - x + 7u) / 8u;                  // blocks of this XCD
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    int lst = 0;
-    if (atomicAdd(&sync[x], 1u) == in_x - 1u) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const unsigned nx = G < 8u ? G : 8u;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      lst = atomicAdd(&sync[8], 1u) == nx - 1u;
-    }
-    last = lst;
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { mx = red_max[i] > mx ? red_max[i] : mx; any |= red_any[i]; }
+    const int gm = sync_gmax(B), par = iteration & 1;
+    S.done_counter[16 + (2 * par) * gm + blockIdx.x] = mx;
+    S.done_counter[16 + (2 * par + 1) * gm + blockIdx.x] = (unsigned)any;
   }
-  __syncthreads();
-  if (last) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    unsigned bm = 0u;
-    int ba = 0;
-    for (unsigned i = threadIdx.x; i < G; i += blockDim.x) {
-      unsigned v = __hip_atomic_load(&sync[16 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      bm = v > bm ? v : bm;
-      ba |= (int)__hip_atomic_load(&sync[16 + G + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Prologue of iteration k >= 1 (one 64-lane wave per workgroup): the stop rule
+// for iteration k-1.  Returns true when the solve has stopped (the wave exits).
+DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim) {
+  if (k == 0) return false;                            // S_0: begin zeroed ctrl[0..1]
+  const dilqr_mpc_ctrl in = S.ctrl[(k - 1) & 1];        // S_{k-1}
+  dilqr_mpc_ctrl out = in;
+  if (!in.stopped) {
+    const int gm = sync_gmax(B), par = (k - 1) & 1;
+    const unsigned* pm = S.done_counter + 16 + (2 * par) * gm;
+    const unsigned* pa = S.done_counter + 16 + (2 * par + 1) * gm;
+    const int lane = threadIdx.x & 63;
+    unsigned mx = 0u;
+    int any = 0;
+    for (int i = lane; i < G; i += 64) {
+      unsigned v = pm[i];
+      mx = v > mx ? v : mx;
+      any |= (int)pa[i];
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-      unsigned o = __shfl_xor(bm, off, 64);
-      bm = o > bm ? o : bm;
-      ba |= __shfl_xor(ba, off, 64);
+      unsigned o = __shfl_xor(mx, off, 64);
+      mx = o > mx ? o : mx;
+      any |= __shfl_xor(any, off, 64);
     }
-    if ((threadIdx.x & 63) == 0) { red_max[w] = bm; red_any[w] = ba; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { bm = red_max[i] > bm ? red_max[i] : bm; ba |= red_any[i]; }
-      bm = red_max[0] > bm ? red_max[0] : bm;
-      ba |= red_any[0];
-      dilqr_mpc_ctrl* ctl = S.ctrl;
-      ctl->iter += 1;
-      ctl->n_not_improved += 1;
-      if (ba) ctl->n_not_improved = 0;
-      if (__uint_as_float(bm) < eps || ctl->n_not_improved > not_improved_lim) ctl->stopped = 1;
-      ctl->max_du_bits = bm;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) __hip_atomic_store(&sync[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    out.iter = in.iter + 1;
+    out.n_not_improved = any ? 0 : in.n_not_improved + 1;     // mpc_explicit.py:264, 279
+    out.max_du_bits = mx;
+    if (__uint_as_float(mx) < eps || out.n_not_improved > not_improved_lim) out.stopped = 1;   // 297-299
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) S.ctrl[k & 1] = out;
+  return out.stopped != 0;
 }
 
 // slot layout: component-major for the thread-per-problem models, the
@@ -1003,7 +999,8 @@ __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float*
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b == 0) {
     dilqr_mpc_ctrl z = {};
-    *S.ctrl = z;
+    S.ctrl[0] = z;
+    S.ctrl[1] = z;
 #pragma unroll
     for (int i = 0; i < 9; ++i) S.done_counter[i] = 0u;
   }
@@ -1605,15 +1602,26 @@ inline bool bad_bounds(const dilqr_bounds& b) {
 
 // the stop-rule kernel with its rows staged in LDS when a block's span fits
 // (64 KiB), else read in place
-inline int launch_norm_control(int TM, int B, float eps, int not_improved_lim, const MpcState& st,
-                               hipStream_t stream) {
+// k_mpc_norm_rows geometry: rows staged in LDS when a block's span fits 64 KiB
+struct NormGeom {
+  int threads, blocks;
+  bool stage;
+};
+inline NormGeom norm_geom(int TM, int B) {
   int threads = 256;
   while (threads > 64 && (size_t)threads * TM * sizeof(float) > 65536) threads >>= 1;
-  const size_t lds = (size_t)threads * TM * sizeof(float);
-  if (lds <= 65536)
-    k_mpc_norm_control<true><<<(B + threads - 1) / threads, threads, lds, stream>>>(TM, B, eps, not_improved_lim, st);
+  const bool stage = (size_t)threads * TM * sizeof(float) <= 65536;
+  if (!stage) threads = 256;
+  return {threads, (B + threads - 1) / threads, stage};
+}
+
+inline int launch_norm_rows(int TM, int B, int iteration, const MpcState& st, hipStream_t stream) {
+  const NormGeom g = norm_geom(TM, B);
+  if (g.stage)
+    k_mpc_norm_rows<true><<<g.blocks, g.threads, (size_t)g.threads * TM * sizeof(float), stream>>>(TM, B, iteration,
+                                                                                                   st);
   else
-    k_mpc_norm_control<false><<<(B + 255) / 256, 256, 0, stream>>>(TM, B, eps, not_improved_lim, st);
+    k_mpc_norm_rows<false><<<g.blocks, g.threads, 0, stream>>>(TM, B, iteration, st);
   return launched();
 }
 
@@ -1936,49 +1944,55 @@ int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float
 
 int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
                        const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
-                       int first, float best_cost_eps, dilqr_mpc_state st, void* stream) {
-  if (T < 1 || B < 0 || max_linesearch_iter < 1 || !theta || !x_init || !C || !c) return DILQR_E_ARG;
+                       int iteration, float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st,
+                       void* stream) {
+  if (T < 1 || B < 0 || max_linesearch_iter < 1 || iteration < 0 || !theta || !x_init || !C || !c) return DILQR_E_ARG;
   if (!al16(x_init) || !al16(C) || !al16(c) || bad_state(st) || bad_bounds(bounds)) return DILQR_E_ARG;
   if (B == 0) return 0;
+  const int m = dilqr_model_num_ctrl(model);
+  if (m < 1) return DILQR_E_SHAPE;
+  const int G = norm_geom(T * m, B).blocks;            // partials of the previous iteration's rows
+  const int lim = not_improved_lim;
   Bounds bd = mkb(bounds);
   bool box = bounds.mode != DILQR_BOUNDS_NONE;
   if (model == DILQR_MODEL_ROCKET) {
     if (box)
       k_mpc_iterate_group<Rocket, GAIN_BOX><<<grid_group(B), 64, 0, S(stream)>>>(
-          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, first, best_cost_eps, st);
+          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim,
+          G, st);
     else
       k_mpc_iterate_group<Rocket, GAIN_UNC><<<grid_group(B), 64, 0, S(stream)>>>(
-          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, first, best_cost_eps, st);
+          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim,
+          G, st);
   } else MODEL_SWITCH_TPP(model, ({
     if (box)
-      k_mpc_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, bd,
-                                                                        linesearch_decay, max_linesearch_iter,
-                                                                        first, best_cost_eps, st);
+      k_mpc_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(
+          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim, G,
+          st);
     else
-      k_mpc_iterate<MD, GAIN_UNC><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, bd,
-                                                                        linesearch_decay, max_linesearch_iter,
-                                                                        first, best_cost_eps, st);
+      k_mpc_iterate<MD, GAIN_UNC><<<grid_for(B), kBlock, 0, S(stream)>>>(
+          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim, G,
+          st);
   }));
   return launched();
 }
 
-int dilqr_mpc_stop_rule_f32(int T, int m, int B, float eps, int not_improved_lim, dilqr_mpc_state st,
-                            void* stream) {
-  if (T < 1 || m < 1 || B < 0 || bad_state(st)) return DILQR_E_ARG;
+int dilqr_mpc_stop_rule_f32(int T, int m, int B, int iteration, dilqr_mpc_state st, void* stream) {
+  if (T < 1 || m < 1 || B < 0 || iteration < 0 || bad_state(st)) return DILQR_E_ARG;
   if (B == 0) return 0;
-  return launch_norm_control(T * m, B, eps, not_improved_lim, st, S(stream));
+  return launch_norm_rows(T * m, B, iteration, st, S(stream));
 }
 
 int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
                           const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
-                          int first, float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st,
+                          int iteration, float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st,
                           void* stream) {
   const int m = dilqr_model_num_ctrl(model);
   if (m < 1) return DILQR_E_SHAPE;
   int e = dilqr_mpc_step_f32(model, T, B, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter,
-                             first, best_cost_eps, st, stream);
+                             iteration, best_cost_eps, eps, not_improved_lim, st, stream);
   if (e) return e;
-  return dilqr_mpc_stop_rule_f32(T, m, B, eps, not_improved_lim, st, stream);
+  return dilqr_mpc_stop_rule_f32(T, m, B, iteration, st, stream);
 }
 
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out, float* u_out,

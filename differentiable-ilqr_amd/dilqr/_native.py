@@ -58,8 +58,8 @@ SIGNATURES = {
     "dilqr_mpc_packed_cost_floats": ([_i, _i], _i),
     "dilqr_mpc_begin_f32": ([_i, _i, _i, _vp, _vp, MpcState, _vp], _i),
     "dilqr_mpc_iterate_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
-    "dilqr_mpc_step_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, MpcState, _vp], _i),
-    "dilqr_mpc_stop_rule_f32": ([_i, _i, _i, _f, _i, MpcState, _vp], _i),
+    "dilqr_mpc_step_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
+    "dilqr_mpc_stop_rule_f32": ([_i, _i, _i, _i, MpcState, _vp], _i),
     "dilqr_mpc_gather_best_f32": ([_i, _i, _i, _i, MpcState, _vp, _vp, _vp], _i),
     "dilqr_implicit_backward_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _vp, _vp, _vp,
                                      _vp, _vp], _i),

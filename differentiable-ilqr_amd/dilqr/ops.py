@@ -153,9 +153,10 @@ class MPCSolve:
         self.du_sq = torch.empty(T, m, B, device=dev)
         self.full_du_norm = torch.empty(B, device=dev)
         self.ws = torch.empty(T * B * ilqr_ws_floats(n, m), device=dev)
-        self.ctrl = torch.zeros(N.CTRL_INTS, dtype=torch.int32, device=dev)
-        # stop-rule sync area: 16 counters + per-block partials (<= ceil(B/64) blocks)
-        self.counter = torch.zeros(16 + 2 * ((B + 63) // 64), dtype=torch.int32, device=dev)
+        self.ctrl = torch.zeros(2 * N.CTRL_INTS, dtype=torch.int32, device=dev)   # ping-pong control state
+        self.last_iteration = -1
+        # stop-rule sync area: 16 words + two planes of per-workgroup partials (<= ceil(B/64))
+        self.counter = torch.zeros(16 + 4 * ((B + 63) // 64), dtype=torch.int32, device=dev)
         # packed symmetric-cost copy for the thread-per-problem fused kernels (d <= 8)
         pk = N.lib().dilqr_mpc_packed_cost_floats(n, m)
         self.Cpk = torch.empty(T * B * pk, device=dev) if n + m <= 8 else None
@@ -176,11 +177,19 @@ class MPCSolve:
         N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), self.state,
                N.stream(x_init.device))
 
-    def iterate(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, first, best_cost_eps, eps,
+    def iterate(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, iteration, best_cost_eps, eps,
                 not_improved_lim):
+        """Iteration `iteration` (0, 1, ...) of the solve started by begin()."""
+        if isinstance(iteration, bool):
+            raise TypeError("iteration is the 0-based iteration index")
         N.call("dilqr_mpc_iterate_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), N.ptr(C),
-               N.ptr(c), bounds, float(decay), int(max_ls), int(first), float(best_cost_eps), float(eps),
+               N.ptr(c), bounds, float(decay), int(max_ls), int(iteration), float(best_cost_eps), float(eps),
                int(min(not_improved_lim, 2 ** 31 - 1)), self.state, N.stream(x_init.device))
+        self.last_iteration = int(iteration)
+
+    def _ctrl_now(self):
+        k = max(self.last_iteration, 0)
+        return self.ctrl.view(2, N.CTRL_INTS)[k & 1]
 
     def gather_best(self):
         x = torch.empty(self.T, self.B, self.n, device=self.Xs.device)
@@ -191,11 +200,13 @@ class MPCSolve:
 
     @property
     def stopped(self):
-        return bool(int(self.ctrl[1].item()))
+        """True once the stop rule fired (the device skips later iterations); the
+        rule for the last launched iteration is applied by the next one."""
+        return bool(int(self._ctrl_now()[1].item()))
 
     @property
     def iterations(self):
-        return int(self.ctrl[0].item())
+        return int(self._ctrl_now()[0].item())
 
 
 def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upper=None, lqr_iter=10,
@@ -212,7 +223,7 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     sv.begin(model_id, theta, x_init, u_init)
     bounds, keep = N.make_bounds(u_lower, u_upper)
     for i in range(lqr_iter):
-        sv.iterate(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i == 0,
+        sv.iterate(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i,
                    best_cost_eps, eps, not_improved_lim)
         if check_every and (i + 1) % check_every == 0 and i + 1 < lqr_iter and sv.stopped:
             break

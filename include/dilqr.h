@@ -199,7 +199,7 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
    into the two free slots, so accepting a step size or taking an iterate as
    the new best (mpc_explicit.py:277-283) moves no data.
    ws: T*B*ceil4(m*n+m+1) floats.  done_counter: the stop rule's sync area of
-   16 + 2*ceil(B/64) uints (its counters are zeroed by begin).
+   16 + 4*ceil(B/64) uints.  ctrl: two dilqr_mpc_ctrl (ping-pong, zeroed by begin).
    Cpk (nullable) + cost_sym [B] (uint8): the solve's packed copy of a
    symmetric cost, T*B*dilqr_mpc_packed_cost_floats(n,m) floats (upper triangle
    of C_t,b row-major, then c_t,b; component-major).  Iteration 0 (first != 0)
@@ -220,23 +220,28 @@ int dilqr_mpc_packed_cost_floats(int n, int m);
 int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init,
                         dilqr_mpc_state st, void* stream);
 
-/* One MPC iteration (mpc_explicit.py:246-299): the fused linearise + Riccati
-   (+pnqp) + line-search kernel on each problem's current slot, best-iterate
-   slot update, then the quirk full_du_norm, best_du and the batch-global stop
-   rule (max du < eps or n_not_improved > lim) on device.  No-op once stopped.
-   first != 0 for iteration 0.  = dilqr_mpc_step_f32 + dilqr_mpc_stop_rule_f32. */
+/* One MPC iteration (mpc_explicit.py:246-299), iteration = 0, 1, ... of the
+   solve.  Two launches: (1) the stop rule for iteration-1 (mpc_explicit.py:264,
+   279, 297-299: max full_du_norm < eps or n_not_improved > not_improved_lim) as
+   the prologue of the fused linearise + Riccati (+pnqp) + line-search kernel on
+   each problem's current slot with the best-iterate slot update; (2) the quirk
+   full_du_norm rows, best_du and per-workgroup partials of this iteration for
+   the next prologue.  Once stopped, iterations are no-ops.  The control state
+   after the decisions for iterations 0..k-1 is in ctrl[k&1] (ctrl points to two
+   dilqr_mpc_ctrl).  = dilqr_mpc_step_f32 + dilqr_mpc_stop_rule_f32. */
 int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const float* x_init,
                           const float* C, const float* c, dilqr_bounds bounds,
-                          float linesearch_decay, int max_linesearch_iter, int first,
+                          float linesearch_decay, int max_linesearch_iter, int iteration,
                           float best_cost_eps, float eps, int not_improved_lim,
                           dilqr_mpc_state st, void* stream);
 /* its two launches, separately (profiling) */
 int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float* x_init,
                        const float* C, const float* c, dilqr_bounds bounds,
-                       float linesearch_decay, int max_linesearch_iter, int first,
-                       float best_cost_eps, dilqr_mpc_state st, void* stream);
-int dilqr_mpc_stop_rule_f32(int T, int m, int B, float eps, int not_improved_lim,
-                            dilqr_mpc_state st, void* stream);
+                       float linesearch_decay, int max_linesearch_iter, int iteration,
+                       float best_cost_eps, float eps, int not_improved_lim,
+                       dilqr_mpc_state st, void* stream);
+int dilqr_mpc_stop_rule_f32(int T, int m, int B, int iteration, dilqr_mpc_state st,
+                            void* stream);
 
 /* Materialise each problem's best trajectory into x_out [T,B,n], u_out [T,B,m]. */
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out,

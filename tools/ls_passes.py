@@ -23,7 +23,7 @@ sv = ops.MPCSolve(T, B, 5, 1, dev)
 nb, _ = N.make_bounds(None, None)
 sv.begin(N.MODEL_CARTPOLE, theta, x0)
 for i in range(10):
-    sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, i == 0, 1e-4, 0.0, 10 ** 9)
+    sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, i, 1e-4, 0.0, 10 ** 9)
     a = sv.alpha.view(-1, 64)
     passes = (a < 1).float()
     print(f"iter {i}: problems with 2 passes {float(passes.mean()):.3f}, waves with 2 passes "
