@@ -512,31 +512,57 @@ struct CostPacked {
   }
 };
 
-template <int n, int m, bool SOA>
-struct SweepIn {
-  static constexpr int d = n + m;
-  float C[d][d], c[d], x[n], u[m];
-  template <class CostT>
-  DEV void load(const CostT& cs, const float* __restrict__ xp, const float* __restrict__ up, int t, int B, int b) {
-    cs.load(C, c, t, B, b); ld_traj<SOA>(x, xp, t, B, b); ld_traj<SOA>(u, up, t, B, b);
+// The box bounds as a compile-time mode (DILQR_BOUNDS_*): scalar bounds are
+// kernel arguments and per-(t,b) bounds are loaded with the step's other data,
+// so no conditional load exists in the step (a conditional load makes the
+// compiler drain every outstanding load, i.e. the prefetch, at the merge).
+template <int m, int BM>
+struct StepBounds {
+  float lo[m], hi[m];
+  DEV void load(const Bounds& bd, int t, int B, int b) {
+    if constexpr (BM == DILQR_BOUNDS_TENSOR) {
+      const size_t tb = (size_t)t * B + b;
+      ld(lo, bd.lo_t + tb * m); ld(hi, bd.hi_t + tb * m);
+    }
+  }
+  DEV float l(const Bounds& bd, int a) const {
+    if constexpr (BM == DILQR_BOUNDS_TENSOR) return lo[a];
+    else return bd.lo;
+  }
+  DEV float h(const Bounds& bd, int a) const {
+    if constexpr (BM == DILQR_BOUNDS_TENSOR) return hi[a];
+    else return bd.hi;
   }
 };
 
-template <int n, int m, int GREC, bool SOA>
+template <int n, int m, bool SOA, int BM>
+struct SweepIn {
+  static constexpr int d = n + m;
+  float C[d][d], c[d], x[n], u[m];
+  StepBounds<m, BM> bnd;
+  template <class CostT>
+  DEV void load(const CostT& cs, const float* __restrict__ xp, const float* __restrict__ up, const Bounds& bd, int t,
+                int B, int b) {
+    cs.load(C, c, t, B, b); ld_traj<SOA>(x, xp, t, B, b); ld_traj<SOA>(u, up, t, B, b); bnd.load(bd, t, B, b);
+  }
+};
+
+template <int n, int m, int GREC, bool SOA, int BM>
 struct FwdIn {
   static constexpr int d = n + m;
   float g[GREC], u[m], C[d][d], c[d], xnext[n];
+  StepBounds<m, BM> bnd;
   template <class CostT>
   DEV void load(const float* __restrict__ grec, const float* __restrict__ up, const CostT& cs,
-                const float* __restrict__ xp, int T, int t, int t1, int B, int b) {
+                const float* __restrict__ xp, const Bounds& bd, int T, int t, int t1, int B, int b) {
     SoaRec<GREC>::load(g, grec, T, t, B, b); ld_traj<SOA>(u, up, t, B, b); cs.load(C, c, t, B, b);
-    ld_traj<SOA>(xnext, xp, t1, B, b);
+    ld_traj<SOA>(xnext, xp, t1, B, b); bnd.load(bd, t, B, b);
   }
 };
 
 // x, u (current trajectory) and the candidate outputs in layout SOA; the gain
 // records in ws and the packed cost are always float4-column.
-template <class Model, int MODE, bool SOA, class CostT>
+template <class Model, int BM, bool SOA, class CostT>
 DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
                      float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
@@ -544,6 +570,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
                      float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
                      float& cost_out, float& alpha_out) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
+  constexpr int MODE = BM == DILQR_BOUNDS_NONE ? GAIN_UNC : GAIN_BOX;
   constexpr int GREC = m * n + m;                    // gain record: K, k (component-major)
   float old_cost = 0.f;                               // the current trajectory's cost, from the sweep
   // ---------------- backward: linearise + Riccati + stage costs of the current trajectory
@@ -551,11 +578,10 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     RiccatiState<n, m> rs;
     rs.init();
     bool sym = true;
-    SweepIn<n, m, SOA> cur, nxt;
-    cur.load(cs, x, u, T - 1, B, b);
+    SweepIn<n, m, SOA, BM> cur, nxt;
+    cur.load(cs, x, u, bd, T - 1, B, b);
     for (int t = T - 1; t >= 0; --t) {
-      size_t tb = (size_t)t * B + b;
-      nxt.load(cs, x, u, t > 0 ? t - 1 : 0, B, b);                     // prefetch step t-1
+      nxt.load(cs, x, u, bd, t > 0 ? t - 1 : 0, B, b);                     // prefetch step t-1
       float tau[d], Ctau[d], cb[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
@@ -593,8 +619,8 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       for (int a = 0; a < m; ++a) {
         zIt[a] = 0.f; lb[a] = 0.f; ub[a] = 0.f;
         if constexpr (MODE == GAIN_BOX) {
-          lb[a] = bound_lo(bd, tb * m + a) - cur.u[a];
-          ub[a] = bound_hi(bd, tb * m + a) - cur.u[a];
+          lb[a] = cur.bnd.l(bd, a) - cur.u[a];
+          ub[a] = cur.bnd.h(bd, a) - cur.u[a];
         }
       }
       float Kt[m][n], kt[m];
@@ -630,14 +656,13 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     st_traj<SOA>(xa_out, xA, 0, B, b);
     if (twoB) st_traj<SOA>(xb_out, xB, 0, B, b);
     float cA = 0.f, cB = 0.f;
-    FwdIn<n, m, GREC, SOA> cur, nxt;
-    cur.load(ws, u, cs, x, T, 0, T > 1 ? 1 : 0, B, b);
+    FwdIn<n, m, GREC, SOA, BM> cur, nxt;
+    cur.load(ws, u, cs, x, bd, T, 0, T > 1 ? 1 : 0, B, b);
     for (int t = 0; t < T; ++t) {
-      const size_t tb = (size_t)t * B + b;
       {
         int t1 = t + 1 < T ? t + 1 : t;                 // prefetch step t+1
         int t2 = t + 2 < T ? t + 2 : t1;
-        nxt.load(ws, u, cs, x, T, t1, t2, B, b);
+        nxt.load(ws, u, cs, x, bd, T, t1, t2, B, b);
       }
       float nuA[m], nuB[m];
 #pragma unroll
@@ -650,8 +675,8 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
         }
         nuA[a] = (sA + cur.u[a]) + aA * cur.g[m * n + a];
         nuB[a] = (sB + cur.u[a]) + aB * cur.g[m * n + a];
-        if (bd.mode != DILQR_BOUNDS_NONE) {
-          const float lo = bound_lo(bd, tb * m + a), hi = bound_hi(bd, tb * m + a);
+        if constexpr (BM != DILQR_BOUNDS_NONE) {
+          const float lo = cur.bnd.l(bd, a), hi = cur.bnd.h(bd, a);
           nuA[a] = eclamp(nuA[a], lo, hi);
           nuB[a] = eclamp(nuB[a], lo, hi);
         }
@@ -708,7 +733,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
   return win;
 }
 
-template <class Model, int MODE>
+template <class Model, int BM>
 __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const float* __restrict__ theta,
                                                          const float* __restrict__ x_init, const float* __restrict__ C,
                                                          const float* __restrict__ c, const float* __restrict__ x,
@@ -728,7 +753,7 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
   // over (x_out, u_out) when it wins
   float* xb = ws + (size_t)T * B * GREC;
   float* ub = xb + (size_t)T * B * n;
-  const int win = ilqr_problem<Model, MODE, false>(T, B, b, md, x_init, CostFull<n + m>{C, c}, nullptr, nullptr, x, u,
+  const int win = ilqr_problem<Model, BM, false>(T, B, b, md, x_init, CostFull<n + m>{C, c}, nullptr, nullptr, x, u,
                                                    bd, decay,
                                             max_ls, ws,
                                             x_out, u_out, xb, ub, du_sq, cost, alpha);
@@ -768,7 +793,7 @@ DEV void free_slots(int cur, int best, int& sa, int& sb) {
   }
 }
 
-template <class Model, int MODE>
+template <class Model, int BM>
 __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const float* __restrict__ theta,
                                                         const float* __restrict__ x_init, const float* __restrict__ C,
                                                         const float* __restrict__ c, Bounds bd, float decay, int max_ls,
@@ -791,11 +816,11 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   // symmetric (per-lane flag; a wave normally takes one side of the branch)
   const CostFull<n + m> full{C, c};
   if (!first && S.Cpk && S.cost_sym[b])
-    win = ilqr_problem<Model, MODE, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
+    win = ilqr_problem<Model, BM, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
                                     S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn,
                                     S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost, alpha);
   else
-    win = ilqr_problem<Model, MODE, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
+    win = ilqr_problem<Model, BM, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
                                     first && S.Cpk ? S.cost_sym : nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd,
                                     decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
                                     S.Us + sb * TBm, S.du_sq, cost, alpha);
@@ -1829,16 +1854,16 @@ int dilqr_ilqr_iterate_f32(int model, int T, int B, const float* theta, const fl
           du_sq, alpha, ctrl);
     return launched();
   }
+#define LAUNCH_IT(BM_)                                                                                              \
+  k_ilqr_iterate<MD, BM_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, x, u, bd, linesearch_decay, \
+                                                                max_linesearch_iter, ws_gains, x_out, u_out, cost,  \
+                                                                du_sq, alpha, ctrl)
   MODEL_SWITCH_TPP(model, ({
-    if (box)
-      k_ilqr_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(
-          T, B, theta, x_init, C, c, x, u, bd, linesearch_decay, max_linesearch_iter, ws_gains, x_out, u_out, cost,
-          du_sq, alpha, ctrl);
-    else
-      k_ilqr_iterate<MD, GAIN_UNC><<<grid_for(B), kBlock, 0, S(stream)>>>(
-          T, B, theta, x_init, C, c, x, u, bd, linesearch_decay, max_linesearch_iter, ws_gains, x_out, u_out, cost,
-          du_sq, alpha, ctrl);
+    if (bounds.mode == DILQR_BOUNDS_TENSOR) LAUNCH_IT(DILQR_BOUNDS_TENSOR);
+    else if (box) LAUNCH_IT(DILQR_BOUNDS_SCALAR);
+    else LAUNCH_IT(DILQR_BOUNDS_NONE);
   }));
+#undef LAUNCH_IT
   return launched();
 }
 
@@ -1964,16 +1989,18 @@ int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float*
       k_mpc_iterate_group<Rocket, GAIN_UNC><<<grid_group(B), 64, 0, S(stream)>>>(
           T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim,
           G, st);
-  } else MODEL_SWITCH_TPP(model, ({
-    if (box)
-      k_mpc_iterate<MD, GAIN_BOX><<<grid_for(B), kBlock, 0, S(stream)>>>(
-          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim, G,
-          st);
-    else
-      k_mpc_iterate<MD, GAIN_UNC><<<grid_for(B), kBlock, 0, S(stream)>>>(
-          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim, G,
-          st);
-  }));
+  } else {
+#define LAUNCH_MPC(BM_)                                                                                      \
+  k_mpc_iterate<MD, BM_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, bd, linesearch_decay, \
+                                                               max_linesearch_iter, iteration, best_cost_eps, eps, \
+                                                               lim, G, st)
+    MODEL_SWITCH_TPP(model, ({
+      if (bounds.mode == DILQR_BOUNDS_TENSOR) LAUNCH_MPC(DILQR_BOUNDS_TENSOR);
+      else if (box) LAUNCH_MPC(DILQR_BOUNDS_SCALAR);
+      else LAUNCH_MPC(DILQR_BOUNDS_NONE);
+    }));
+#undef LAUNCH_MPC
+  }
   return launched();
 }
 
