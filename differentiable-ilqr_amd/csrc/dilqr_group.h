@@ -41,31 +41,30 @@ struct GroupLds {
   float tau[W];
 };
 
-// gains from the u-rows of Q, identical in every lane (modes as RiccatiState)
+// Gains from the u-rows of Q (modes as RiccatiState::step), distributed over
+// the group: lane j solves right-hand side j — Q_ux column j for j < n, q_u for
+// j = n — against the same m x m matrix (elimination and pivots depend only on
+// the matrix, so each column's arithmetic is exactly the multi-RHS solve's).
+// pnqp (box mode) needs all of q_u and runs in every lane.  Lane j < n returns
+// K[:, j] in col; lane n returns k.
 template <int n, int m, int MODE>
-DEV void group_gains(const float (&Quu)[m][m], const float (&Qux)[m][n], const float (&qu)[m],
-                     const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&K)[m][n],
-                     float (&k)[m], float (&prev_k)[m], bool& have_prev, int& n_qp) {
+DEV void group_gains_col(int j, const float (&Quu)[m][m], const float (&rhs)[m], const float (&qu)[m],
+                         const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&col)[m],
+                         float (&prev_k)[m], bool& have_prev, int& n_qp) {
   if constexpr (MODE == GAIN_UNC || MODE == GAIN_CHOL) {
-    float A[m][m], X[m][n + 1];
+    float A[m][m], X[m][1];
 #pragma unroll
     for (int a = 0; a < m; ++a) {
 #pragma unroll
       for (int b = 0; b < m; ++b) A[a][b] = Quu[a][b] + ((MODE == GAIN_CHOL && a == b) ? 1e-6f : 0.f);
-#pragma unroll
-      for (int j = 0; j < n; ++j) X[a][j] = Qux[a][j];
-      X[a][n] = qu[a];
+      X[a][0] = rhs[a];
     }
-    if constexpr (MODE == GAIN_CHOL) chol_solve<m, n + 1>(A, X);
-    else gauss_solve<m, n + 1>(A, X);
+    if constexpr (MODE == GAIN_CHOL) chol_solve<m, 1>(A, X);
+    else gauss_solve<m, 1>(A, X);
 #pragma unroll
-    for (int a = 0; a < m; ++a) {
-#pragma unroll
-      for (int j = 0; j < n; ++j) K[a][j] = -X[a][j];
-      k[a] = -X[a][n];
-    }
+    for (int a = 0; a < m; ++a) col[a] = -X[a][0];
   } else if constexpr (MODE == GAIN_ZERO_I) {
-    float A[m][m], X[m][n + 1];
+    float A[m][m], X[m][1];
 #pragma unroll
     for (int a = 0; a < m; ++a) {
       bool Ia = zI[a] != 0.f;
@@ -74,36 +73,26 @@ DEV void group_gains(const float (&Quu)[m][m], const float (&Qux)[m][n], const f
         bool fr = (zI[a] == 0.f) && (zI[b] == 0.f);
         A[a][b] = (fr ? Quu[a][b] : 0.f) + ((a == b && Ia) ? 1e-8f : 0.f);
       }
-#pragma unroll
-      for (int j = 0; j < n; ++j) X[a][j] = Ia ? 0.f : Qux[a][j];
-      X[a][n] = Ia ? 0.f : qu[a];
+      X[a][0] = Ia ? 0.f : rhs[a];
     }
-    gauss_solve<m, n + 1>(A, X);
+    gauss_solve<m, 1>(A, X);
 #pragma unroll
-    for (int a = 0; a < m; ++a) {
-#pragma unroll
-      for (int j = 0; j < n; ++j) K[a][j] = -X[a][j];
-      k[a] = -X[a][n];
-    }
-  } else {                                        // GAIN_BOX: pnqp
+    for (int a = 0; a < m; ++a) col[a] = -X[a][0];
+  } else {                                        // GAIN_BOX: pnqp, then the free-block solve
     float x[m], If[m], Hf[m][m];
 #pragma unroll
     for (int a = 0; a < m; ++a) x[a] = prev_k[a];
     int it = pnqp<m>(Quu, qu, lb, ub, have_prev, x, If, Hf);
     n_qp += 1 + it;
 #pragma unroll
-    for (int a = 0; a < m; ++a) { k[a] = x[a]; prev_k[a] = x[a]; }
+    for (int a = 0; a < m; ++a) prev_k[a] = x[a];
     have_prev = true;
-    float X[m][n];
+    float X[m][1];
 #pragma unroll
-    for (int a = 0; a < m; ++a)
+    for (int a = 0; a < m; ++a) X[a][0] = If[a] != 0.f ? rhs[a] : 0.f;
+    gauss_solve<m, 1>(Hf, X);
 #pragma unroll
-      for (int j = 0; j < n; ++j) X[a][j] = If[a] != 0.f ? Qux[a][j] : 0.f;
-    gauss_solve<m, n>(Hf, X);
-#pragma unroll
-    for (int a = 0; a < m; ++a)
-#pragma unroll
-      for (int j = 0; j < n; ++j) K[a][j] = -X[a][j];
+    for (int a = 0; a < m; ++a) col[a] = j < n ? -X[a][0] : x[a];
   }
 }
 
@@ -147,27 +136,36 @@ DEV void group_riccati_step(GroupLds<n, m>& L, int r, const float (&Crow)[n + m]
     L.Qu[r - n][GroupLds<n, m>::W] = qr;
   }
   __syncthreads();
-  float Quu[m][m], Qux[m][n], qu[m];
+  float Quu[m][m], qu[m], rhs[m];
+  const int jc = r <= n ? r : n;                 // this lane's right-hand side (lanes > n repeat k's)
 #pragma unroll
   for (int a = 0; a < m; ++a) {
 #pragma unroll
     for (int b = 0; b < m; ++b) Quu[a][b] = L.Qu[a][n + b];
-#pragma unroll
-    for (int j = 0; j < n; ++j) Qux[a][j] = L.Qu[a][j];
     qu[a] = L.Qu[a][GroupLds<n, m>::W];
+    rhs[a] = jc < n ? L.Qu[a][jc] : qu[a];
   }
-  group_gains<n, m, MODE>(Quu, Qux, qu, zI, lb, ub, K, k, prev_k, have_prev, n_qp);
-  // K[a][r] (this lane's column) from registers without a runtime index: the
-  // group leader publishes K, k in LDS
-  if ((r & (kG - 1)) == 0) {
+  float col[m];
+  group_gains_col<n, m, MODE>(jc, Quu, rhs, qu, zI, lb, ub, col, prev_k, have_prev, n_qp);
+  if (r < n) {
 #pragma unroll
-    for (int a = 0; a < m; ++a) {
+    for (int a = 0; a < m; ++a) L.Kk[a][r] = col[a];
+  } else if (r == n) {
 #pragma unroll
-      for (int j = 0; j < n; ++j) L.Kk[a][j] = K[a][j];
-      L.Kk[a][GroupLds<n, m>::W] = k[a];
-    }
+    for (int a = 0; a < m; ++a) L.Kk[a][GroupLds<n, m>::W] = col[a];
   }
   __syncthreads();
+#pragma unroll
+  for (int a = 0; a < m; ++a) {
+#pragma unroll
+    for (int jj = 0; jj < n; ++jj) K[a][jj] = L.Kk[a][jj];
+    k[a] = L.Kk[a][GroupLds<n, m>::W];
+  }
+  float Qux[m][n];
+#pragma unroll
+  for (int a = 0; a < m; ++a)
+#pragma unroll
+    for (int jj = 0; jj < n; ++jj) Qux[a][jj] = L.Qu[a][jj];
   if (r < n) {
     float Kc[m];
 #pragma unroll

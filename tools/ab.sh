@@ -7,7 +7,7 @@ L=differentiable-ilqr_amd/dilqr/libdilqr.so
 for r in $(seq ${1:-3}); do
   for v in A B; do
     cp ab/libdilqr_$v.so $L
-    out=$(timeout -k 10 120 python bench.py --kernels-only ${BENCH_ARGS:-}) || exit 1
+    out=$(timeout -k 10 300 python ${AB_CMD:-bench.py --kernels-only ${BENCH_ARGS:-}} | tail -1) || exit 1
     echo "$v $out"
   done
 done
