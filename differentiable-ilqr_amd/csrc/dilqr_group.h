@@ -39,6 +39,7 @@ struct GroupLds {
   float Qu[m][W + 4];                          // u rows of Q, q_u at [.][W]
   float Kk[m][W + 4];                          // gains K, k at [.][W]
   float tau[W];
+  float tau2[W];                               // the paired line search's second candidate
 };
 
 // Gains from the u-rows of Q (modes as RiccatiState::step), distributed over
@@ -391,6 +392,103 @@ DEV float group_forward_pass(GroupLds<n, m>& L, const Model* md, const float* __
   return cst;
 }
 
+// Two step sizes rolled out together (the fused MPC kernel's paired line
+// search, see ilqr_problem): candidates A (alpha aA) and B (aB, if twoB) share
+// the step's loads; each keeps its own state component, controls and cost.
+template <int n, int m, int GREC, class Model>
+DEV void group_forward_pair(GroupLds<n, m>& L, const Model& md, int T, int B, int b, int r, bool valid, float aA,
+                            float aB, bool twoB, const float* __restrict__ x_init, const float* __restrict__ C,
+                            const float* __restrict__ c, const float* __restrict__ x, const float* __restrict__ u,
+                            const float* __restrict__ grec, const Bounds& bd, float* __restrict__ xa_out,
+                            float* __restrict__ ua_out, float* __restrict__ xb_out, float* __restrict__ ub_out,
+                            float* __restrict__ du_sq, float& cA, float& cB, float& old_cost) {
+  constexpr int d = n + m;
+  float xA = (r < n) ? x_init[(size_t)b * n + r] : 0.f, xB = xA;
+  float dA = 0.f, dB = 0.f;
+  if (valid && r < n) {
+    xa_out[(size_t)b * n + r] = xA;
+    if (twoB) xb_out[(size_t)b * n + r] = xB;
+  }
+  float sA = 0.f, sB = 0.f, oldc = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const size_t tb = (size_t)t * B + b;
+    const float* rec = grec + tb * GREC;
+    float ut[m], kt[m], Kc[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      kt[a] = rec[m * n + a];
+      Kc[a] = r < n ? rec[a * n + r] : 0.f;
+      ut[a] = u[tb * m + a];
+    }
+    oldc += rec[m * n + m];
+    float nuA[m], nuB[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      const float pa = group_sum(Kc[a] * dA), pb = group_sum(Kc[a] * dB);
+      nuA[a] = (pa + ut[a]) + aA * kt[a];
+      nuB[a] = (pb + ut[a]) + aB * kt[a];
+      if (bd.mode != DILQR_BOUNDS_NONE) {
+        const float lo = bound_lo(bd, tb * m + a), hi = bound_hi(bd, tb * m + a);
+        nuA[a] = eclamp(nuA[a], lo, hi);
+        nuB[a] = eclamp(nuB[a], lo, hi);
+      }
+    }
+    float nrA = 0.f, nrB = 0.f, uur = 0.f;
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      nrA = (r == n + a) ? nuA[a] : nrA;
+      nrB = (r == n + a) ? nuB[a] : nrB;
+      uur = (r == n + a) ? ut[a] : uur;
+    }
+    if (valid && r >= n && r < d) {
+      ua_out[tb * m + (r - n)] = nrA;
+      if (twoB) ub_out[tb * m + (r - n)] = nrB;
+      if (du_sq) {
+        float e = uur - nrA;
+        du_sq[((size_t)t * m + (r - n)) * B + b] = e * e;
+      }
+    }
+    if (r < n) { L.tau[r] = xA; L.tau2[r] = xB; }
+    __syncthreads();
+    float fA[n], fB[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) { fA[i] = L.tau[i]; fB[i] = L.tau2[i]; }
+    __syncthreads();
+    float pA = 0.f, pB = 0.f;
+    if (r < d) {
+      float Crow[d];
+      ld(Crow, C + (tb * d + r) * d);
+      const float cr = c[tb * d + r];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < n; ++j) { s1 += Crow[j] * fA[j]; s2 += Crow[j] * fB[j]; }
+#pragma unroll
+      for (int a = 0; a < m; ++a) { s1 += Crow[n + a] * nuA[a]; s2 += Crow[n + a] * nuB[a]; }
+      const float tA = r < n ? xA : nrA, tB = r < n ? xB : nrB;
+      pA = 0.5f * (tA * s1) + tA * cr;
+      pB = 0.5f * (tB * s2) + tB * cr;
+    }
+    sA += group_sum(pA);
+    sB += group_sum(pB);
+    if (t < T - 1 && r < n) {
+      const float xo = x[(tb + B) * n + r];
+      const float nA = md.forward_row(r, fA, nuA);
+      dA = nA - xo;
+      xA = nA;
+      if (valid) xa_out[(tb + B) * n + r] = xA;
+      if (twoB) {
+        const float nB = md.forward_row(r, fB, nuB);
+        dB = nB - xo;
+        xB = nB;
+        if (valid) xb_out[(tb + B) * n + r] = xB;
+      }
+    }
+  }
+  cA = sA;
+  cB = sB;
+  old_cost = oldc;
+}
+
 // the line search's accept test (lqr_step_explicit.py:244-252) for a group.  The
 // 16 lanes of a group hold the same cost, so `done` is group-uniform; the wave
 // keeps looping until every group accepted (its barriers stay balanced), and a
@@ -469,8 +567,9 @@ DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b
                             const Model& md, const float* __restrict__ x_init, const float* __restrict__ C,
                             const float* __restrict__ c, const float* __restrict__ x, const float* __restrict__ u,
                             const Bounds& bd, float decay, int max_ls, float* __restrict__ ws,
-                            float* __restrict__ x_out, float* __restrict__ u_out, float* __restrict__ du_sq,
-                            float& cost_out, float& alpha_out) {
+                            float* __restrict__ x_out, float* __restrict__ u_out, float* __restrict__ xb_out,
+                            float* __restrict__ ub_out, float* __restrict__ du_sq, float& cost_out, float& alpha_out,
+                            int& win_out) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
   constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
   constexpr int W = GroupLds<n, m>::W;
@@ -542,16 +641,40 @@ DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b
   }
   // ---------------- forward line search
   float alpha = 1.f, cost = 0.f, old_cost = 0.f;
-  for (int ls = 0; ls < max_ls; ++ls) {
-    float oldc;
-    cost = group_forward_pass<n, m, GREC>(L, &md, nullptr, nullptr, T, B, b, r, valid, alpha, x_init, C, c, x, u,
-                                          nullptr, nullptr, ws, bd, nullptr, x_out, u_out, ls == 0 ? du_sq : nullptr,
-                                          &oldc);
-    if (ls == 0) old_cost = oldc;
-    if (group_ls_done(cost, old_cost, ls, max_ls, valid, alpha, decay)) break;
+  int win = 0;
+  if (xb_out) {
+    // passes 2r and 2r+1 together (first accepted wins = the sequential search);
+    // the wave leaves when every group accepted
+    bool done = false;
+    for (int p = 0; p < max_ls; p += 2) {
+      const bool twoB = p + 1 < max_ls;
+      float cA, cB, oc;
+      const float aA = alpha, aB = alpha * decay;
+      // a group that already accepted keeps rolling (its barriers) but writes nothing
+      group_forward_pair<n, m, GREC>(L, md, T, B, b, r, valid && !done, aA, aB, twoB, x_init, C, c, x, u, ws, bd,
+                                     x_out,
+                                     u_out, xb_out, ub_out, p == 0 ? du_sq : nullptr, cA, cB, oc);
+      if (p == 0) old_cost = oc;
+      if (!done) {
+        if (!(cA > old_cost) || p == max_ls - 1) { cost = cA; alpha = aA; win = 0; done = true; }
+        else if (!(cB > old_cost) || p + 1 == max_ls - 1) { cost = cB; alpha = aB; win = 1; done = true; }
+        else alpha = aB * decay;
+      }
+      if (__all(done || !valid)) break;
+    }
+  } else {
+    for (int ls = 0; ls < max_ls; ++ls) {
+      float oldc;
+      cost = group_forward_pass<n, m, GREC>(L, &md, nullptr, nullptr, T, B, b, r, valid, alpha, x_init, C, c, x, u,
+                                            nullptr, nullptr, ws, bd, nullptr, x_out, u_out,
+                                            ls == 0 ? du_sq : nullptr, &oldc);
+      if (ls == 0) old_cost = oldc;
+      if (group_ls_done(cost, old_cost, ls, max_ls, valid, alpha, decay)) break;
+    }
   }
   cost_out = cost;
   alpha_out = alpha;
+  win_out = win;
 }
 
 }  // namespace dilqr

@@ -855,8 +855,9 @@ __global__ void __launch_bounds__(64) k_ilqr_iterate_group(int T, int B, const f
   const int b = valid ? b0 : B - 1;          // idle groups shadow problem B-1 (same wave), writing nothing
   Model md; md.load(theta);
   float cost, alpha;
+  int win;
   group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, x, u, bd, decay, max_ls, ws, x_out,
-                                  u_out, du_sq, cost, alpha);
+                                  u_out, nullptr, nullptr, du_sq, cost, alpha, win);
   if (valid && r == 0) {
     cost_out[b] = cost;
     alpha_out[b] = alpha;
@@ -881,11 +882,14 @@ __global__ void __launch_bounds__(64) k_mpc_iterate_group(int T, int B, const fl
   Model md; md.load(theta);
   const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
   const int cur = S.slot[b], best = S.slot[B + b];
-  int nw, unused;
-  free_slots(cur, best, nw, unused);
+  int sa, sb;
+  free_slots(cur, best, sa, sb);
   float cost, alpha;
+  int win;
   group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, S.Xs + cur * TBn, S.Us + cur * TBm,
-                                  bd, decay, max_ls, S.ws, S.Xs + nw * TBn, S.Us + nw * TBm, S.du_sq, cost, alpha);
+                                  bd, decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
+                                  S.Us + sb * TBm, S.du_sq, cost, alpha, win);
+  const int nw = win ? sb : sa;
   if (valid && r == 0) {
     S.cost[b] = cost;
     S.alpha[b] = alpha;
