@@ -387,6 +387,35 @@ __global__ void __launch_bounds__(kBlock) k_quirk_norm(int TM, int B, const floa
   out[r] = sqrtf(s);
 }
 
+// ============================================================ standalone pnqp
+// pnqp.py:5-82 for one problem per lane (the reference at batch size 1):
+// min 1/2 x^T H x + q^T x, lower <= x <= upper, warm start x_init (nullable:
+// the unconstrained solve, pnqp.py:14-19).  Outputs x, the free mask If, the
+// masked matrix H_ of the last iteration (pnqp.py:44-48) and the iteration
+// index at exit (pnqp.py:59 / 82).
+template <int m>
+__global__ void __launch_bounds__(kBlock) k_pnqp(int B, const float* __restrict__ H, const float* __restrict__ q,
+                                                 Bounds bd, const float* __restrict__ x_init, float* __restrict__ x,
+                                                 float* __restrict__ If, float* __restrict__ Hf_out,
+                                                 int* __restrict__ n_iter) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float Hr[m][m], qr[m], lb[m], ub[m], xr[m], Ir[m], Hf[m][m];
+  ld2(Hr, H + (size_t)b * m * m);
+  ld(qr, q + (size_t)b * m);
+#pragma unroll
+  for (int a = 0; a < m; ++a) {
+    lb[a] = bound_lo(bd, (long long)b * m + a);
+    ub[a] = bound_hi(bd, (long long)b * m + a);
+    xr[a] = x_init ? x_init[(size_t)b * m + a] : 0.f;
+  }
+  const int it = pnqp<m>(Hr, qr, lb, ub, x_init != nullptr, xr, Ir, Hf);
+  st(x + (size_t)b * m, xr);
+  if (If) st(If + (size_t)b * m, Ir);
+  if (Hf_out) st2(Hf_out + (size_t)b * m * m, Hf);
+  if (n_iter) n_iter[b] = it;
+}
+
 // ============================================================ fused iLQR iteration
 // One MPC iteration body (mpc_explicit.py:249-263) for ONE problem (this lane):
 // linearise at the current trajectory on the fly, Riccati sweep (+pnqp), the
@@ -1823,6 +1852,22 @@ int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* th
         T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter, x_out,
         u_out, cost, du_sq, alpha);
   }));
+  return launched();
+}
+
+int dilqr_pnqp_f32(int m, int B, const float* H, const float* q, dilqr_bounds bounds, const float* x_init, float* x,
+                   float* If, float* Hfree, int* n_iter, void* stream) {
+  if (m < 1 || B < 0 || !H || !q || !x) return DILQR_E_ARG;
+  if (bounds.mode == DILQR_BOUNDS_NONE || bad_bounds(bounds)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  Bounds bd = mkb(bounds);
+  switch (m) {
+    case 1: k_pnqp<1><<<grid_for(B), kBlock, 0, S(stream)>>>(B, H, q, bd, x_init, x, If, Hfree, n_iter); break;
+    case 2: k_pnqp<2><<<grid_for(B), kBlock, 0, S(stream)>>>(B, H, q, bd, x_init, x, If, Hfree, n_iter); break;
+    case 3: k_pnqp<3><<<grid_for(B), kBlock, 0, S(stream)>>>(B, H, q, bd, x_init, x, If, Hfree, n_iter); break;
+    case 4: k_pnqp<4><<<grid_for(B), kBlock, 0, S(stream)>>>(B, H, q, bd, x_init, x, If, Hfree, n_iter); break;
+    default: return DILQR_E_SHAPE;
+  }
   return launched();
 }
 

@@ -47,6 +47,7 @@ SIGNATURES = {
                                 _vp], _i),
     "dilqr_lqr_forward_f32": ([_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds,
                                _vp, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "dilqr_pnqp_f32": ([_i, _i, _vp, _vp, Bounds, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_quirk_norm_f32": ([_i, _i, _i, _vp, _vp, _vp], _i),
     "dilqr_ilqr_iterate_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _f, _i, _vp, _vp, _vp, _vp,
                                 _vp, _vp, _vp, _vp], _i),

@@ -92,6 +92,23 @@ def lqr_forward(model_id, theta, x_init, C, c, x, u, K, k, F=None, f=None, u_low
     return nx, nu, cost, du_sq, alpha
 
 
+def pnqp(H, q, lower, upper, x_init=None):
+    """pnqp.py:5-82 per problem -> (x [B,m], H_ [B,m,m], If [B,m], n_iter [B]).
+    lower/upper: floats or [B,m] tensors.  The reference's batched call couples
+    the Armijo loop across the batch; this is the reference at batch size 1."""
+    B, m = q.shape
+    H, q, x_init = _f32(H), _f32(q), _f32(x_init)
+    bounds, keep = N.make_bounds(lower, upper)
+    x = torch.empty(B, m, device=q.device)
+    If = torch.empty(B, m, device=q.device)
+    Hf = torch.empty(B, m, m, device=q.device)
+    it = torch.empty(B, dtype=torch.int32, device=q.device)
+    N.call("dilqr_pnqp_f32", m, B, N.ptr(H), N.ptr(q), bounds, N.ptr(x_init), N.ptr(x), N.ptr(If), N.ptr(Hf),
+           N.ptr(it), N.stream(q.device))
+    del keep
+    return x, Hf, If, it
+
+
 def quirk_norm(du_sq):
     """lqr_step_explicit.py:245-247 norm over the re-viewed [T,m,B] buffer."""
     T, m, B = du_sq.shape

@@ -137,6 +137,18 @@ typedef struct dilqr_mpc_ctrl {
   int pad[3];
 } dilqr_mpc_ctrl;
 
+/* Projected-Newton box QP, pnqp.py:5-82, per problem (the reference at batch
+   size 1; its batched call couples the Armijo exits across the batch):
+   min 1/2 x^T H x + q^T x, lower <= x <= upper.  H [B,m,m], q [B,m], bounds
+   scalar or [B,m] (mode NONE is an error), x_init [B,m] nullable (then the
+   unconstrained solve, pnqp.py:14-19).  Outputs x [B,m]; If [B,m] free mask,
+   Hfree [B,m,m] the masked matrix of the last iteration (pnqp.py:44-48; the
+   reference returns it for m=1 and its LU for m>1) and n_iter [B] the iteration
+   index at exit (pnqp.py:59/82), each nullable.  m <= 4. */
+int dilqr_pnqp_f32(int m, int B, const float* H, const float* q, dilqr_bounds bounds,
+                   const float* x_init, float* x, float* If, float* Hfree, int* n_iter,
+                   void* stream);
+
 /* One fused iLQR iteration for a model (not LINDX): linearise on the fly,
    Riccati sweep (+pnqp), old cost, line-search rollout.  Reads the current
    trajectory (x,u), writes the new one (x_out,u_out), cost [B], du_sq [T,m,B],

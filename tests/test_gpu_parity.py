@@ -513,3 +513,24 @@ def test_fused_iteration_vs_oracle(model, bounds, decay, mls):
     assert np.median(cerr[same]) < 1e-5 and np.max(cerr[same]) < 1e-3
     assert relerr(cpu(nu)[:, same], uo[:, same]) < 1e-3
     assert relerr(cpu(nx)[:, same], xo[:, same]) < 1e-3
+
+
+# ------------------------------------------------------------------ standalone pnqp (a4)
+@pytest.mark.parametrize("m", [1, 3])
+def test_pnqp_standalone_vs_golden(golden, m):
+    """dilqr_pnqp_f32 against the reference's pnqp called per problem (golden
+    x_pp / it_pp), and with a warm start and scalar bounds against the oracle's
+    per-problem restatement (x, free mask, masked H, iteration index)."""
+    from dilqr import ops
+    g = golden("pnqp_f64")
+    H, q, lo, hi, x0 = (g[f"m{m}_{k}"] for k in ("H", "q", "lo", "hi", "x0"))
+    x, Hf, If, it = ops.pnqp(gpu(H), gpu(q), gpu(lo), gpu(hi))
+    assert relerr(cpu(x), g[f"m{m}_x_pp"]) < 1e-4
+    assert np.mean(cpu(it) == g[f"m{m}_it_pp"]) > 0.95       # exit index: fp32 near-ties at 1e-4
+    x2, Hf2, If2, it2 = ops.pnqp(gpu(H), gpu(q), -0.7, 0.7, x_init=gpu(x0))
+    xo, Hfo, Ifo, ito = olqr.pnqp(H, q, -0.7, 0.7, x_init=x0, per_problem=True)
+    assert relerr(cpu(x2), xo) < 1e-4
+    same = cpu(it2) == ito
+    assert np.mean(same) > 0.95
+    assert np.array_equal(cpu(If2)[same], Ifo[same])
+    assert relerr(cpu(Hf2)[same], Hfo[same]) < 1e-5
