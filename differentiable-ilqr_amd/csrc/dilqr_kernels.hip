@@ -38,6 +38,49 @@ __global__ void __launch_bounds__(kBlock) k_dynamics(int N, const float* __restr
   st(out + (size_t)i * n, o);
 }
 
+// Vector-Jacobian product of forward() (the sysid loss's backward,
+// il_exp.py:338-347, which the reference gets from autograd): per row,
+// g_theta = gout^T df/dtheta, g_x = gout^T df/dx, g_u = gout^T df/du, all at the
+// CLAMPED u (df/du = 0 where the clamp is active, as autograd through
+// torch.clamp gives).  g_theta is written per row; the caller sums.
+template <class Model>
+__global__ void __launch_bounds__(kBlock) k_dynamics_vjp(int N, const float* __restrict__ theta,
+                                                         const float* __restrict__ x, const float* __restrict__ u,
+                                                         const float* __restrict__ gout, float* __restrict__ gtheta,
+                                                         float* __restrict__ gx, float* __restrict__ gu) {
+  constexpr int n = Model::N, m = Model::M, p = Model::P;
+  using D2 = typename D2Of<Model>::type;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  Model md; md.load(theta);
+  float xi[n], ui[m], uc[m], go[n];
+  ld(xi, x + (size_t)i * n); ld(ui, u + (size_t)i * m); ld(go, gout + (size_t)i * n);
+#pragma unroll
+  for (int a = 0; a < m; ++a) uc[a] = fminf(fmaxf(ui[a], -Model::ULIM), Model::ULIM);
+  float D[n][n + m], Ft[n][p];
+  md.jacobian(xi, uc, D);
+  D2::f_theta(theta, xi, uc, Ft);
+  float gt[p], gxi[n], gui[m];
+#pragma unroll
+  for (int k = 0; k < p; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < n; ++r) s += go[r] * Ft[r][k];
+    gt[k] = s;
+  }
+#pragma unroll
+  for (int j = 0; j < n + m; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < n; ++r) s += go[r] * D[r][j];
+    if (j < n) gxi[j] = s;
+    else gui[j - n] = (ui[j - n] >= -Model::ULIM && ui[j - n] <= Model::ULIM) ? s : 0.f;
+  }
+  st(gtheta + (size_t)i * p, gt);
+  if (gx) st(gx + (size_t)i * n, gxi);
+  if (gu) st(gu + (size_t)i * m, gui);
+}
+
 template <class Model>
 __global__ void __launch_bounds__(kBlock) k_linear_dyn(int N, const float* __restrict__ theta,
                                                        const float* __restrict__ x, const float* __restrict__ u,
@@ -1730,6 +1773,15 @@ int dilqr_dynamics_f32(int model, int N, const float* theta, const float* x, con
   if (N < 0 || !theta || !x || !u || !out) return DILQR_E_ARG;
   if (N == 0) return 0;
   MODEL_SWITCH(model, (k_dynamics<MD><<<grid_for(N), kBlock, 0, S(stream)>>>(N, theta, x, u, out)));
+  return launched();
+}
+
+int dilqr_dynamics_vjp_f32(int model, int N, const float* theta, const float* x, const float* u, const float* gout,
+                           float* gtheta, float* gx, float* gu, void* stream) {
+  if (N < 0 || !theta || !x || !u || !gout || !gtheta) return DILQR_E_ARG;
+  if (N == 0) return 0;
+  MODEL_SWITCH_TPP(model, (k_dynamics_vjp<MD><<<grid_for(N), kBlock, 0, S(stream)>>>(N, theta, x, u, gout, gtheta,
+                                                                                       gx, gu)));
   return launched();
 }
 

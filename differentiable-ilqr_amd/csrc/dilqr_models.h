@@ -14,6 +14,7 @@ namespace dilqr {
 struct Pendulum {
   static constexpr int N = 3, M = 1, P = 3;
   static constexpr float DT = 0.05f;
+  static constexpr float ULIM = 2.0f;      // forward() clamps u to [-ULIM, ULIM]
   float g, m, l;
   DEV void load(const float* __restrict__ th) { g = th[0]; m = th[1]; l = th[2]; }
 
@@ -60,6 +61,7 @@ struct Pendulum {
 struct Cartpole {
   static constexpr int N = 5, M = 1, P = 4;
   static constexpr float DT = 0.05f;
+  static constexpr float ULIM = 100.0f;
   float g, mc, mp, l;
   DEV void load(const float* __restrict__ th) { g = th[0]; mc = th[1]; mp = th[2]; l = th[3]; }
 

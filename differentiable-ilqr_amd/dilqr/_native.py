@@ -40,6 +40,7 @@ SIGNATURES = {
     "dilqr_model_num_params": ([_i], _i),
     "dilqr_model_num_ctrl": ([_i], _i),
     "dilqr_dynamics_f32": ([_i, _i, _vp, _vp, _vp, _vp, _vp], _i),
+    "dilqr_dynamics_vjp_f32": ([_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_linear_dyn_f32": ([_i, _i, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_rollout_f32": ([_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_linearize_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),

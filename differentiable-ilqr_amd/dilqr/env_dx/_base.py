@@ -6,6 +6,31 @@ from torch import nn
 from .. import _native as N
 
 
+class _DynamicsFn(torch.autograd.Function):
+    """forward() with the gradient autograd gives the reference (its forward is
+    eager torch): dilqr_dynamics_f32 forward, dilqr_dynamics_vjp_f32 backward."""
+
+    @staticmethod
+    def forward(ctx, x, u, theta, model_id):
+        x, u, th = x.detach().contiguous(), u.detach().contiguous(), theta.detach().contiguous()
+        out = torch.empty_like(x)
+        N.call("dilqr_dynamics_f32", model_id, x.shape[0], N.ptr(th), N.ptr(x), N.ptr(u), N.ptr(out),
+               N.stream(x.device))
+        ctx.save_for_backward(x, u, th)
+        ctx.model_id = model_id
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, u, th = ctx.saved_tensors
+        gout = gout.detach().float().contiguous()
+        gth = torch.empty(x.shape[0], th.shape[0], device=x.device)
+        gx, gu = torch.empty_like(x), torch.empty_like(u)
+        N.call("dilqr_dynamics_vjp_f32", ctx.model_id, x.shape[0], N.ptr(th), N.ptr(x), N.ptr(u), N.ptr(gout),
+               N.ptr(gth), N.ptr(gx), N.ptr(gu), N.stream(x.device))
+        return gx, gu, gth.sum(0), None
+
+
 class HipDynamics(nn.Module):
     model_id = None
     n_state = n_ctrl = None
@@ -20,11 +45,17 @@ class HipDynamics(nn.Module):
         squeeze = x.ndimension() == 1
         if squeeze:
             x, u = x.unsqueeze(0), u.unsqueeze(0)
-        x = x.detach().contiguous()
-        u = u.detach().contiguous()
-        out = torch.empty_like(x)
-        N.call("dilqr_dynamics_f32", self.model_id, x.shape[0], N.ptr(self._theta(x)), N.ptr(x), N.ptr(u),
-               N.ptr(out), N.stream(x.device))
+        p = self.params if isinstance(self.params, torch.Tensor) else torch.tensor(self.params)
+        needs_grad = torch.is_grad_enabled() and (x.requires_grad or u.requires_grad or p.requires_grad)
+        if needs_grad:
+            th = p.to(device=x.device, dtype=torch.float32)
+            out = _DynamicsFn.apply(x.float(), u.float(), th, self.model_id)
+        else:
+            x = x.detach().contiguous()
+            u = u.detach().contiguous()
+            out = torch.empty_like(x)
+            N.call("dilqr_dynamics_f32", self.model_id, x.shape[0], N.ptr(self._theta(x)), N.ptr(x), N.ptr(u),
+                   N.ptr(out), N.stream(x.device))
         return out.squeeze(0) if squeeze else out
 
     def get_linear_dyn(self, x, u):

@@ -74,6 +74,15 @@ int dilqr_model_num_ctrl(int model);
 int dilqr_dynamics_f32(int model, int N, const float* theta, const float* x,
                        const float* u, float* out, void* stream);
 
+/* Vector-Jacobian product of dilqr_dynamics_f32 (the reference obtains it from
+   autograd through forward(), e.g. the sysid loss, il_exp.py:338-347): per row
+   gtheta [N,p] = gout^T df/dtheta (per row; sum over rows for the parameter
+   gradient), gx [N,n] = gout^T df/dx, gu [N,m] = gout^T df/du (0 where the
+   model's control clamp is active), each at the clamped u.  gx, gu nullable.
+   Models: pendulum, cartpole. */
+int dilqr_dynamics_vjp_f32(int model, int N, const float* theta, const float* x,
+                           const float* u, const float* gout, float* gtheta, float* gx,
+                           float* gu, void* stream);
 /* D = d f / d [x;u] at the unclamped u, [N,n,n+m].  Replaces get_linear_dyn:
    cartpole.py:790-839, pendulum.py:444-475, rocket.py:324-426. */
 int dilqr_linear_dyn_f32(int model, int N, const float* theta, const float* x,

@@ -1,0 +1,86 @@
+"""The IL loop counterpart (SURVEY.md §8 f #1-2): dataset I/O without
+unpickling, IL_Env.mpc / populate_data, and the sysid / empc training steps."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+CART_PKL = os.path.join(GOLDEN, "cartpole_dataset.pkl")      # the reference's data/cartpole.pkl
+PEND_PKL = os.path.join(GOLDEN, "pendulum_dataset.pkl")      # the reference's data/pendulum.pkl
+
+
+@pytest.mark.parametrize("env,path", [("cartpole", CART_PKL), ("pendulum", PEND_PKL)])
+def test_dataset_loader_matches_golden(golden, env, path):
+    """load_il_dataset walks the pickle opcodes (nothing is unpickled) and
+    returns the same arrays the golden generator extracted."""
+    from dilqr import il
+    d = il.load_il_dataset(path)
+    g = golden("datasets")
+    assert d["env"] == env
+    for k in ("train_data", "val_data", "test_data", "params"):
+        np.testing.assert_array_equal(d[k].numpy(), g[f"{env}_{k}"].astype(np.float32))
+    for k in ("lqr_iter", "mpc_T", "linesearch_decay", "max_linesearch_iter", "mpc_eps", "lower", "upper"):
+        assert float(d[k]) == float(g[f"{env}_{k}"]), k
+
+
+@pytest.mark.gpu
+def test_il_env_reproduces_dataset():
+    """IL_Env.mpc from the dataset's own initial states reproduces the expert
+    controls of data/cartpole.pkl (T=35, lqr_iter=100, eps=1e-4, bounds 100)."""
+    from dilqr import il
+    env = il.IL_Env.from_dataset(CART_PKL, device="cuda")
+    data = torch.cat([env.train_data, env.val_data, env.test_data]).cuda()
+    n = env.true_dx.n_state
+    q, p = env.true_dx.get_true_obj()
+    with torch.no_grad():
+        x, u = env.mpc(env.true_dx, data[:, 0, :n].contiguous(), q.cuda(), p.cuda())
+    ref_u = data[:, :, n:].transpose(0, 1)
+    err = (u - ref_u).abs().max() / ref_u.abs().max()
+    assert float(err) < 1e-3, float(err)
+
+
+@pytest.mark.gpu
+def test_dynamics_vjp_vs_finite_differences():
+    """Autograd through HipDynamics.forward (dilqr_dynamics_vjp_f32) vs central
+    differences of the fp64 oracle model, incl. rows with a clamped control."""
+    from dilqr.env_dx.cartpole import CartpoleDx
+    from oracle import models as om
+    rng = np.random.RandomState(0)
+    N = 64
+    th = rng.uniform(-np.pi, np.pi, N)
+    x = np.stack([rng.normal(size=N), rng.normal(size=N), np.cos(th), np.sin(th), rng.normal(size=N)], 1)
+    u = rng.uniform(-150, 150, (N, 1))                   # some beyond the +-100 clamp
+    w = rng.normal(size=(N, 5))
+    params = torch.tensor((9.8, 1.0, 0.1, 0.5), device="cuda", requires_grad=True)
+    xt = torch.tensor(x, dtype=torch.float32, device="cuda", requires_grad=True)
+    ut = torch.tensor(u, dtype=torch.float32, device="cuda", requires_grad=True)
+    loss = (CartpoleDx(params)(xt, ut) * torch.tensor(w, dtype=torch.float32, device="cuda")).sum()
+    loss.backward()
+    p0 = np.array((9.8, 1.0, 0.1, 0.5))
+
+    def L(pp, xx, uu):
+        return float((om.Cartpole.forward(xx, uu, pp) * w).sum())
+    eps = 1e-6
+    g_fd = np.array([(L(p0 + eps * e, x, u) - L(p0 - eps * e, x, u)) / (2 * eps) for e in np.eye(4)])
+    assert np.allclose(params.grad.cpu().numpy(), g_fd, rtol=2e-3, atol=1e-3)
+    gu_fd = np.array([(L(p0, x, u + eps * np.eye(1)[0]) - L(p0, x, u - eps * np.eye(1)[0])) / (2 * eps)])
+    assert abs(float(ut.grad.sum()) - gu_fd[0]) < 1e-2 * max(1.0, abs(gu_fd[0]))
+    assert float(ut.grad[np.abs(u[:, 0]) > 100].abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,kw", [("sysid", {}), ("empc", {"learn_dx": True}), ("empc", {"learn_cost": True})])
+def test_il_trainer_runs_and_learns(mode, kw):
+    """A few epochs of the reference's training loop on data/pendulum.pkl
+    (20 training trajectories): finite losses, the loss falls, parameters move."""
+    from dilqr import il
+    env = il.IL_Env.from_dataset(PEND_PKL, device="cuda")
+    env.lqr_iter = 30
+    tr = il.ILTrainer(env, mode=mode, n_batch=10, n_train=20, **kw)
+    h = tr.fit(6)
+    train = np.array([r[1 if mode != "sysid" else 2] for r in h["train"]])
+    assert np.isfinite(train).all() and len(h["val_test"]) == 6
+    assert train[-2:].mean() < train[:2].mean()
