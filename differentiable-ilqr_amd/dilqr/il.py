@@ -17,6 +17,7 @@ import warnings
 import numpy as np
 import torch
 from torch import optim
+from torch.utils.data import DataLoader, TensorDataset
 
 from .definitions import QuadCost
 from .env_dx.cartpole import CartpoleDx
@@ -183,11 +184,14 @@ class ILTrainer:
         self.cost_update_q = False
         self.epoch = 0
 
-    # -- il_exp.py:432-439
-    def _split(self, data):
+    # -- il_exp.py:432-439 (the same DataLoader, so shuffling draws the global
+    # generator exactly as the reference's loop does)
+    def _loader(self, data, shuffle=False):
         data = data.to(self.device)
         xs, us = data[:, :, :self.n_state], data[:, :, -self.n_ctrl:]
-        return xs[:, 0], xs, us
+        xinits = xs[:, 0]
+        ds = TensorDataset(xinits, xs, us, torch.arange(0, xinits.shape[0], device=self.device))
+        return DataLoader(ds, batch_size=self.n_batch, shuffle=shuffle)
 
     def _dx(self):
         return self.env.true_dx.__class__(self.env_params)
@@ -200,25 +204,22 @@ class ILTrainer:
 
     def fit(self, n_epoch):
         env, T = self.env, self.env.mpc_T
-        xi_tr, xs_tr, us_tr = self._split(env.train_data[:self.n_train])
-        xi_va, _, us_va = self._split(env.val_data)
-        xi_te, _, us_te = self._split(env.test_data)
-        if not hasattr(self, "train_warmstart"):
-            self.train_warmstart = torch.zeros(xi_tr.shape[0], T, self.n_ctrl, device=self.device)
-            self.val_warmstart = torch.zeros(xi_va.shape[0], T, self.n_ctrl, device=self.device)
-            self.test_warmstart = torch.zeros(xi_te.shape[0], T, self.n_ctrl, device=self.device)
-        g = torch.Generator().manual_seed(self.seed)
+        if self.epoch == 0:
+            torch.manual_seed(self.seed)                      # il_exp.py:184
+            self.train = self._loader(env.train_data[:self.n_train], shuffle=True)
+            self.val = self._loader(env.val_data)
+            self.test = self._loader(env.test_data)
+            self.train_warmstart = torch.zeros(len(self.train.dataset), T, self.n_ctrl, device=self.device)
+            self.val_warmstart = torch.zeros(len(self.val.dataset), T, self.n_ctrl, device=self.device)
+            self.test_warmstart = torch.zeros(len(self.test.dataset), T, self.n_ctrl, device=self.device)
+        n_batches = len(self.train)
         for _ in range(n_epoch):
             i = self.epoch
             if i > 0 and i % self.ROUND_ROBIN == 0:
                 self.cost_update_q = not self.cost_update_q
             if i % self.RESTART_WARMSTART_EVERY == 0:
                 self.train_warmstart.zero_(); self.val_warmstart.zero_(); self.test_warmstart.zero_()
-            perm = torch.randperm(xi_tr.shape[0], generator=g).to(self.device)     # DataLoader(shuffle=True)
-            n_batches = (xi_tr.shape[0] + self.n_batch - 1) // self.n_batch
-            for j in range(n_batches):
-                idxs = perm[j * self.n_batch:(j + 1) * self.n_batch]
-                xinits, xs, us = xi_tr[idxs], xs_tr[idxs], us_tr[idxs]
+            for j, (xinits, xs, us, idxs) in enumerate(self.train):
                 dx = self._dx()
                 q, p = self._qp()
                 nom_x, nom_u = env.mpc(dx, xinits, q, p, u_init=self.train_warmstart[idxs].transpose(0, 1))
@@ -241,24 +242,26 @@ class ILTrainer:
                         self.learn_p.grad.zero_()
                     else:
                         self.learn_q_logit.grad.zero_()
-                self.opt.step()
+                # dx_hist.csv / cost_hist.csv rows: the parameters this step used
                 self.history["params"].append(self.env_params.detach().cpu().numpy().copy())
-            val = self.dataset_loss(xi_va, us_va, self.val_warmstart)
-            test = self.dataset_loss(xi_te, us_te, self.test_warmstart)
+                if self.learn_cost:
+                    q, p = self._qp()
+                    self.history.setdefault("cost", []).append(torch.cat((q, p)).detach().cpu().numpy().copy())
+                self.opt.step()
+            val = self.dataset_loss(self.val, self.val_warmstart)
+            test = self.dataset_loss(self.test, self.test_warmstart)
             self.history["val_test"].append([i, val, test])
             self.epoch += 1
         return self.history
 
     @torch.no_grad()
-    def dataset_loss(self, xinits, us, warmstart):
-        """il_exp.py:440-495 (one batch of size n_batch at a time)."""
+    def dataset_loss(self, loader, warmstart):
+        """il_exp.py:440-495."""
         losses = []
-        for s in range(0, xinits.shape[0], self.n_batch):
-            idxs = torch.arange(s, min(s + self.n_batch, xinits.shape[0]), device=self.device)
+        for xinits, xs, us, idxs in loader:
             q, p = self._qp()
-            _, pred_u = self.env.mpc(self._dx(), xinits[idxs], q, p, u_init=warmstart[idxs].transpose(0, 1))
+            _, pred_u = self.env.mpc(self._dx(), xinits, q, p, u_init=warmstart[idxs].transpose(0, 1))
             pred_u = pred_u.transpose(0, 1)
             warmstart[idxs] = pred_u
-            losses.append((us[idxs] - pred_u).pow(2).mean(dim=1))
+            losses.append((us - pred_u).pow(2).mean(dim=1))
         return float(torch.cat(losses).mean())
-

@@ -484,11 +484,73 @@ def case_datasets():
     save("datasets", **out)
 
 
+# --------------------------------------------------------------------------
+# I. the IL training loop (il_exp.py:183-429) on a reference dataset
+# --------------------------------------------------------------------------
+IL_CASES = {
+    # name: (dataset, mode, learn_cost, learn_dx, n_train, n_batch, n_epoch, lqr_iter)
+    "pend_sysid": ("pendulum", "sysid", False, True, 10, 5, 3, None),
+    "pend_empc_dx": ("pendulum", "empc", False, True, 10, 5, 2, 30),
+    "pend_empc_cost": ("pendulum", "empc", True, False, 10, 5, 2, 30),
+}
+
+
+def case_il():
+    """IL_Exp(...).run() with its dataset handed over WITHOUT unpickling: the
+    IL_Env is rebuilt from the statically parsed dataset and il_exp's `pkl.load`
+    is pointed at it (pkl.dump of the best model is a no-op).  setproctitle and
+    IPython (absent here) are stand-in modules used only by il_exp's process
+    title and excepthook.  The losses/parameter histories come from the CSV
+    files run() writes."""
+    print("I. il loop")
+    import csv
+    import shutil
+    import tempfile
+    st = types.ModuleType("setproctitle")
+    st.setproctitle = lambda *a, **k: None
+    sys.modules.setdefault("setproctitle", st)
+    ip, ipc, ub = types.ModuleType("IPython"), types.ModuleType("IPython.core"), types.ModuleType("IPython.core.ultratb")
+    ub.FormattedTB = lambda *a, **k: sys.excepthook
+    ip.core, ipc.ultratb = ipc, ub
+    for k, v in (("IPython", ip), ("IPython.core", ipc), ("IPython.core.ultratb", ub)):
+        sys.modules.setdefault(k, v)
+    import il_env
+    import il_exp
+    out = {}
+    for name, (ds, mode, lc, ldx, n_train, n_batch, n_epoch, lqr_iter) in IL_CASES.items():
+        scalars, tensors = parse_dataset(os.path.join(REF, "data", ds + ".pkl"))
+        env = il_env.IL_Env(ds, lqr_iter=lqr_iter or int(scalars["lqr_iter"]), mpc_T=int(scalars["mpc_T"]))
+        for k in ("train_data", "val_data", "test_data"):
+            setattr(env, k, torch.tensor(tensors[k], dtype=torch.float32))
+        il_exp.pkl = types.SimpleNamespace(load=lambda f, _e=env: _e, dump=lambda *a, **k: None)
+        work = tempfile.mkdtemp()
+        try:
+            exp = il_exp.IL_Exp(data=os.path.join(REF, "data", ds + ".pkl"), work=work, save=os.path.join(work, "s"),
+                                n_batch=n_batch, mode=mode, learn_cost=lc, learn_dx=ldx, no_cuda=True, seed=5,
+                                n_epoch=n_epoch, n_train=n_train, device="cpu")
+            with contextlib.redirect_stdout(io.StringIO()):
+                exp.run()
+            rd = lambda f: np.array([[float(v) for v in row] for row in list(csv.reader(open(os.path.join(exp.save, f))))[1:]])
+            out[f"{name}_train"] = rd("train_losses.csv")
+            out[f"{name}_val_test"] = rd("val_test_losses.csv")
+            if ldx:
+                out[f"{name}_dx_hist"] = np.array([[float(v) for v in row] for row in csv.reader(open(os.path.join(exp.save, "dx_hist.csv")))])
+            if lc:
+                out[f"{name}_cost_hist"] = np.array([[float(v) for v in row] for row in csv.reader(open(os.path.join(exp.save, "cost_hist.csv")))])
+            print(f"  {name}: ok")
+        except Exception as e:          # the reference's own failure is recorded, not hidden
+            print(f"  {name}: reference raised {type(e).__name__}: {e}")
+            out[f"{name}_error"] = np.array(f"{type(e).__name__}: {e}")
+        finally:
+            shutil.rmtree(work, ignore_errors=True)
+    save("il", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["models", "riccati", "pnqp", "lqrstep", "mpc", "adjoint", "implicit",
-                             "datasets"]
+                             "datasets", "il"]
     table = {"models": case_models, "riccati": case_riccati, "pnqp": case_pnqp,
              "lqrstep": case_lqrstep, "mpc": case_mpc, "adjoint": case_classic_adjoint,
-             "implicit": case_implicit, "datasets": case_datasets}
+             "implicit": case_implicit, "datasets": case_datasets, "il": case_il}
     for w in which:
         table[w]()
