@@ -149,6 +149,7 @@ def secondary_configs(dev):
     from dilqr import _native as N
     from dilqr import ops
     from dilqr.implicit import implicit_backward
+    from dilqr.env_dx.cartpole import CartpoleDx
     out = {}
     stream = torch.cuda.current_stream(dev)
     s = N.stream(dev)
@@ -205,7 +206,6 @@ def secondary_configs(dev):
     g = torch.Generator(device=dev).manual_seed(1)
     wx = torch.zeros(T, B, n, device=dev)
     wu = torch.randn(T, B, m, device=dev, generator=g)                 # loss = sum(u * w), SURVEY §8(d)
-    from dilqr.env_dx.cartpole import CartpoleDx
     cart = CartpoleDx()
     ib = lambda _r: implicit_backward(cart, wx, wu, C, c, None, None, x, u, K, -10.0, 10.0, None)
     ib(0)
@@ -213,6 +213,36 @@ def secondary_configs(dev):
     out["config4_implicit_backward"] = {"kernel": "k_implicit_backward<Cartpole> (dC, dc, dtheta)",
                                         "avg_ms": ms, "problems_per_s": B / (ms * 1e-3), "batch": B, "T": T,
                                         "bounds": "+-10"}
+    del sv, C, c
+    # ---- one empc training step of the IL loop (il_exp.py:297-352):
+    # MPC forward (lqr_iter 100, eps 1e-4, bounds +-100, T=35) + im_loss backward into the
+    # dynamics parameters, cartpole, 4096 problems from config-2 initial states
+    from dilqr import il
+    env = il.IL_Env("cartpole", lqr_iter=100, mpc_T=35, device=dev)
+    Bi = 4096
+    xi = torch.tensor(make_problems(Bi, seed=2)[0], device=dev)
+    params = torch.tensor((9.8, 3.0, 0.1, 1.0), device=dev, requires_grad=True)
+    qi, pi_ = env.true_dx.get_true_obj()
+    qi, pi_ = qi.to(dev), pi_.to(dev)
+    target = torch.zeros(35, Bi, 1, device=dev)
+
+    def il_step():
+        params.grad = None
+        _, uu = env.mpc(CartpoleDx(params), xi, qi, pi_)
+        loss = (target - uu).pow(2).mean()
+        loss.backward()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        il_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            il_step()
+        torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / 3
+    out["il_empc_step_cartpole"] = {"ms_per_step": ms, "batch": Bi, "T": 35, "lqr_iter_max": 100,
+                                    "what": "MPC forward to the stop rule + implicit backward into theta"}
     return out
 
 
