@@ -263,11 +263,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # BENCH_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one GPU
+    # (the timing all-reduce then runs on the host); the driver's runs use RCCL
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank if backend == "nccl" else local_rank % max(ndev, 1)
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            tdist.init_process_group(backend)
+    dev = torch.device("cuda", dev_index)
 
     from dilqr import _native as N
     from dilqr import ops
@@ -311,7 +319,7 @@ def main():
         tdist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
     assert bool(torch.isfinite(sv.best_cost).all()), "non-finite costs"
