@@ -317,6 +317,122 @@ class Rocket(_Model):
         return [xi + di * dt for xi, di in zip(xs, deriv)]
 
     @classmethod
+    def get_matrices(cls, x, u, params=None):
+        """rocket.py:258-261 with the reference's build_batched_* tensors.  D,
+        x_grad_theta and x_grad_utm1 equal the derivatives (sympy); the builders
+        of D_grad_params (738-820), D_grad_x (677-735), D_grad_u (633-675) and
+        x_grad_xtm1 (541-631) are sparse closed forms that do NOT follow the
+        derivative of D (most entries sit at shifted indices), and are restated
+        here entry by entry as the reference writes them."""
+        D, _Dp, _Dx, _Du, fp, _xx, x_u = super().get_matrices(x, u, params)
+        Jx, Jy, Jz, mass, l = (x.dtype.type(v) for v in (params if params is not None else cls.default_params))
+        dt = x.dtype.type(cls.dt)
+        N = x.shape[0]
+        z = lambda *shape: np.zeros((N,) + shape, x.dtype)
+        ux, uy, uz = u[:, 0], u[:, 1], u[:, 2]
+        q0, q1, q2, q3 = x[:, 6], x[:, 7], x[:, 8], x[:, 9]
+        wx, wy, wz = x[:, 10], x[:, 11], x[:, 12]
+        # ---- x_grad_xtm1 (rocket.py:541-631)
+        xx = z(13, 13)
+        for i in range(13):
+            xx[:, i, i] = 1.0
+        xx[:, 3, 0] = dt; xx[:, 4, 1] = dt; xx[:, 5, 2] = dt
+        xx[:, 6, 3] = dt * ((uz * 2 * q2 - uy * 2 * q3)) / mass
+        xx[:, 6, 4] = dt * ((ux * 2 * q3 - uz * 2 * q1)) / mass
+        xx[:, 6, 5] = dt * ((uy * 2 * q1 - ux * 2 * q2)) / mass
+        xx[:, 6, 10] = dt * 0.5 * wx; xx[:, 6, 11] = dt * 0.5 * wy; xx[:, 6, 12] = dt * 0.5 * wz
+        xx[:, 7, 3] = dt * ((uy * 2 * q2 + uz * 2 * q3)) / mass
+        xx[:, 7, 4] = dt * ((ux * 2 * q2 - uy * 4 * q1 - uz * 2 * q0)) / mass
+        xx[:, 7, 5] = dt * ((ux * 2 * q3 + uy * 2 * q0 - uz * 4 * q1)) / mass
+        xx[:, 7, 10] = -dt * 0.5 * wx; xx[:, 7, 11] = -dt * 0.5 * wz; xx[:, 7, 12] = dt * 0.5 * wy
+        xx[:, 8, 3] = dt * ((uy * 2 * q1 - ux * 4 * q2 + uz * 2 * q0)) / mass
+        xx[:, 8, 4] = dt * ((ux * 2 * q1 + uz * 2 * q3)) / mass
+        xx[:, 8, 5] = dt * ((uy * 2 * q3 - ux * 2 * q0 - uz * 4 * q2)) / mass
+        xx[:, 8, 10] = -dt * 0.5 * wy; xx[:, 8, 11] = dt * 0.5 * wz; xx[:, 8, 12] = -dt * 0.5 * wx
+        xx[:, 9, 3] = dt * ((uz * 2 * q1 - ux * 4 * q3 - uy * 2 * q0)) / mass
+        xx[:, 9, 4] = dt * ((ux * 2 * q0 - uy * 4 * q3 + uz * 2 * q2)) / mass
+        xx[:, 9, 5] = dt * ((ux * 2 * q1 + uy * 2 * q2)) / mass
+        xx[:, 9, 10] = -dt * 0.5 * wz; xx[:, 9, 11] = -dt * 0.5 * wy; xx[:, 9, 12] = dt * 0.5 * wx
+        xx[:, 10, 6] = -dt * 0.5 * q1; xx[:, 10, 7] = dt * 0.5 * q0
+        xx[:, 10, 8] = dt * 0.5 * q3; xx[:, 10, 9] = -dt * 0.5 * q2
+        xx[:, 10, 11] = -dt * ((wz * Jx - wz * Jz)) / Jy
+        xx[:, 10, 12] = -dt * ((wy * Jy - wy * Jx)) / Jz
+        xx[:, 11, 6] = -dt * 0.5 * q2; xx[:, 11, 7] = -dt * 0.5 * q3
+        xx[:, 11, 8] = dt * 0.5 * q0; xx[:, 11, 9] = dt * 0.5 * q1
+        xx[:, 11, 10] = -dt * ((wz * Jz - wz * Jy)) / Jx
+        xx[:, 11, 12] = -dt * ((wx * Jy - wx * Jx)) / Jz
+        xx[:, 12, 6] = -dt * 0.5 * q3; xx[:, 12, 7] = dt * 0.5 * q2
+        xx[:, 12, 8] = -dt * 0.5 * q1; xx[:, 12, 9] = dt * 0.5 * q0
+        xx[:, 12, 10] = -dt * ((wy * Jz - wy * Jy)) / Jx
+        xx[:, 12, 11] = -dt * ((wx * Jx - wx * Jz)) / Jy
+        # ---- D_grad_u (rocket.py:633-675)
+        Du = z(13, 16, 3)
+        Du[:, 5, 5, 0] = dt * (2 * q3 / mass); Du[:, 5, 6, 0] = -dt * (2 * q2 / mass)
+        Du[:, 6, 5, 1] = -dt * (2 * q3 / mass); Du[:, 6, 7, 1] = dt * (2 * q1 / mass)
+        Du[:, 7, 5, 2] = dt * (2 * q2 / mass); Du[:, 7, 6, 2] = -dt * (2 * q1 / mass)
+        # ---- D_grad_x (rocket.py:677-735)
+        Dx = z(13, 16, 13)
+        Dx[:, 5, 5, 6] = -dt * (2 * uz / mass) * q3
+        Dx[:, 5, 6, 6] = dt * 0.5; Dx[:, 5, 7, 6] = dt * 0.5; Dx[:, 5, 8, 6] = dt * 0.5
+        Dx[:, 5, 5, 7] = dt * (2 * uy / mass) * q3
+        Dx[:, 6, 5, 7] = dt * (2 * ux / mass) * q2 + dt * (2 * uy / mass) * q1
+        Dx[:, 5, 5, 8] = dt * (2 * uz / mass) * q0 - dt * (2 * ux / mass) * q3
+        Dx[:, 6, 5, 8] = dt * (2 * ux / mass) * q1 - dt * (4 * uy / mass) * q0 - dt * (2 * uz / mass) * q3
+        Dx[:, 5, 5, 9] = -dt * (2 * uy / mass) * q0 + dt * (2 * ux / mass) * q1
+        Dx[:, 6, 5, 9] = dt * (2 * ux / mass) * q0 - dt * (2 * uz / mass) * q2
+        Dx[:, 9, 9, 10] = -dt * 0.5
+        Dx[:, 10, 10, 10] = -dt * (Jy - Jx) / Jz * wy
+        Dx[:, 10, 11, 10] = dt * (Jx - Jz) / Jy * wz
+        Dx[:, 9, 10, 11] = dt * 0.5
+        Dx[:, 11, 10, 11] = -dt * (Jy - Jx) / Jz * wx
+        Dx[:, 11, 12, 11] = dt * (Jz - Jy) / Jx * wz
+        Dx[:, 9, 11, 12] = dt * 0.5
+        Dx[:, 9, 12, 12] = -dt * 0.5
+        Dx[:, 12, 11, 12] = -dt * (Jx - Jz) / Jy * wy
+        Dx[:, 12, 10, 12] = dt * (Jz - Jy) / Jx * wx
+        # ---- D_grad_params (rocket.py:738-820)
+        Dp = z(13, 16, 5)
+        Dp[:, 11, 10, 0] = -dt * (wz / Jy); Dp[:, 12, 10, 0] = dt * (wy / Jz)
+        Dp[:, 11, 12, 0] = dt * ((wy * Jz - wy * Jy) / Jx ** 2); Dp[:, 12, 11, 0] = dt * (wx / Jz)
+        Dp[:, 11, 10, 1] = dt * ((wz * Jx - wz * Jz) / Jy ** 2); Dp[:, 12, 10, 1] = -dt * (wy / Jz)
+        Dp[:, 11, 13, 1] = dt * (wz / Jx); Dp[:, 12, 11, 1] = -dt * (wx / Jz)
+        Dp[:, 11, 14, 1] = dt * (wy / Jx)
+        Dp[:, 12, 12, 1] = dt * ((wx * Jx - wx * Jz) / Jy ** 2)
+        Dp[:, 11, 15, 1] = -dt * ((l / 2) / Jy ** 2)
+        Dp[:, 11, 10, 2] = dt * (wz / Jy)
+        Dp[:, 12, 10, 2] = dt * ((wy * Jy - wy * Jx) / Jz ** 2)
+        Dp[:, 11, 13, 2] = -dt * (wz / Jx)
+        Dp[:, 12, 11, 2] = dt * ((wx * Jy - wx * Jx) / Jz ** 2)
+        Dp[:, 11, 14, 2] = -dt * (wy / Jx)
+        Dp[:, 12, 12, 2] = dt * (wx / Jy)
+        Dp[:, 12, 14, 2] = dt * ((l / 2) / Jz ** 2)
+        m2 = mass ** 2
+        Dp[:, 3, 13, 3] = -dt * (1 - 2 * (q2 ** 2 + q3 ** 2)) / m2
+        Dp[:, 4, 13, 3] = -dt * (2 * (q1 * q2 + q0 * q3)) / m2
+        Dp[:, 5, 13, 3] = -dt * (2 * (q1 * q3 - q0 * q2)) / m2
+        Dp[:, 3, 14, 3] = -dt * (2 * (q1 * q2 - q0 * q3)) / m2
+        Dp[:, 4, 14, 3] = -dt * (1 - 2 * (q1 ** 2 + q3 ** 2)) / m2
+        Dp[:, 5, 14, 3] = -dt * (2 * (q2 * q3 + q0 * q1)) / m2
+        Dp[:, 3, 15, 3] = -dt * (2 * (q1 * q3 + q0 * q2)) / m2
+        Dp[:, 4, 15, 3] = -dt * (2 * (q2 * q3 - q0 * q1)) / m2
+        Dp[:, 5, 15, 3] = -dt * (1 - 2 * (q1 ** 2 + q2 ** 2)) / m2
+        Dp[:, 3, 13, 3] += -dt * ((uz * 2 * q2 - uy * 2 * q3)) / m2
+        Dp[:, 4, 13, 3] += -dt * ((ux * 2 * q3 - uz * 2 * q1)) / m2
+        Dp[:, 5, 13, 3] += -dt * ((uy * 2 * q1 - ux * 2 * q2)) / m2
+        Dp[:, 3, 14, 3] += -dt * ((uy * 2 * q2 + uz * 2 * q3)) / m2
+        Dp[:, 4, 14, 3] += -dt * ((ux * 2 * q2 - uy * 4 * q1 - uz * 2 * q0)) / m2
+        Dp[:, 5, 14, 3] += -dt * ((ux * 2 * q3 + uy * 2 * q0 - uz * 4 * q1)) / m2
+        Dp[:, 3, 15, 3] += -dt * ((uy * 2 * q1 - ux * 4 * q2 + uz * 2 * q0)) / m2
+        Dp[:, 4, 15, 3] += -dt * ((ux * 2 * q1 + uz * 2 * q3)) / m2
+        Dp[:, 5, 15, 3] += -dt * ((uy * 2 * q3 - ux * 2 * q0 - uz * 4 * q2)) / m2
+        Dp[:, 3, 15, 3] += -dt * (uz * 2 * q1 - ux * 4 * q3 - uy * 2 * q0) / m2
+        Dp[:, 4, 15, 3] += -dt * (ux * 2 * q0 - uy * 4 * q3 + uz * 2 * q2) / m2
+        Dp[:, 5, 15, 3] += -dt * (ux * 2 * q1 + uy * 2 * q2) / m2
+        Dp[:, 11, 15, 4] = dt * 0.5 / Jy ** 2
+        Dp[:, 12, 14, 4] = -dt * 0.5 / Jz ** 2
+        return D, Dp, Dx, Du, fp, xx, x_u
+
+    @classmethod
     def true_obj(cls):
         """rocket.py:212-232, including its double application of tilt_penalty
         (tilt_Q is pre-multiplied at rocket.py:77 and again at 225)."""

@@ -405,7 +405,10 @@ def case_implicit():
     print("G. implicit backward")
     cases = {"cart_unc": ("cartpole", 10, 4, None, "cart_unc"),
              "cart_box": ("cartpole", 10, 4, (-5.0, 5.0), "cart_box10"),
-             "pend_box": ("pendulum", 10, 4, (-2.0, 2.0), "pend_box")}
+             "pend_box": ("pendulum", 10, 4, (-2.0, 2.0), "pend_box"),
+             # rocket: the reference's D_x/D_u/D_params/x_xtm1 builders (rocket.py:541-820)
+             "rock_unc": ("rocket", 10, 4, None, "rocket_unc"),
+             "rock_box": ("rocket", 10, 4, (-10.0, 10.0), "rocket_unc")}
     for dt in (torch.float64, torch.float32):
         with default_dtype(dt):
             out = {}
@@ -425,6 +428,9 @@ def case_implicit():
                 x, u = np_(x), np_(u)
                 wx = rng.normal(size=x.shape)
                 wu = rng.normal(size=u.shape)
+                # MKL's batched getrf hangs on the rocket's 160x160 KKT systems with
+                # 8 threads in this image (lqr_step_explicit.py:570); one thread is fine
+                torch.set_num_threads(1 if mname == "rocket" else 8)
                 dQ, dP, dth, F, f = implicit_once(mname, T, B, bounds, x, u, x0, Q, P, wx, wu, dt)
                 # per-problem d theta: weight only problem j
                 dth_b = []

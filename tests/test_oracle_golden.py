@@ -30,12 +30,9 @@ def test_model_forward_and_jacobian(golden, name, prec, tol):
     assert rel(M.get_linear_dyn(x, u), g[f"{name}_D"]) < tol * 10
 
 
-ROCKET_2ND = pytest.param("rocket", marks=pytest.mark.xfail(
-    reason="rocket.py build_batched_* second-order builders are not yet restated "
-           "(rocket implicit backward is SURVEY.md §8(f) next #3)", strict=True))
 
 
-@pytest.mark.parametrize("name", ["pendulum", "cartpole", ROCKET_2ND])
+@pytest.mark.parametrize("name", ["pendulum", "cartpole", "rocket"])
 def test_model_get_matrices(golden, name):
     g = golden("models_f64")
     M = MODELS[name]
@@ -47,7 +44,7 @@ def test_model_get_matrices(golden, name):
         assert rel(val, ref) < 1e-10, key
 
 
-@pytest.mark.parametrize("name", ["pendulum", "cartpole", ROCKET_2ND])
+@pytest.mark.parametrize("name", ["pendulum", "cartpole", "rocket"])
 def test_model_grad_input(golden, name):
     g = golden("models_f64")
     M = MODELS[name]
@@ -192,7 +189,8 @@ def test_classic_adjoint(golden, tag, bounds):
 
 # ---------------------------------------------------------------- DiLQR implicit backward
 IMPLICIT = {"cart_unc": ("cartpole", None), "cart_box": ("cartpole", (-5.0, 5.0)),
-            "pend_box": ("pendulum", (-2.0, 2.0))}
+            "pend_box": ("pendulum", (-2.0, 2.0)), "rock_unc": ("rocket", None),
+            "rock_box": ("rocket", (-10.0, 10.0))}
 
 
 @pytest.mark.parametrize("tag", list(IMPLICIT))
