@@ -44,6 +44,27 @@ extern "C" void MODEL##_f_theta(const float* th, const float* x, const float* u,
 }
 WRAP(Pendulum, 4, 3, 1, 3)
 WRAP(Cartpole, 6, 5, 1, 4)
+// rocket: per-lane pieces, assembled over all lanes
+extern "C" void Rocket_pieces(const float* th, const float* x, const float* u, const float* lam, float* mcol,
+                              float* mp, float* xx, float* xth) {
+  using R = dilqr::gen::RocketD2;
+  float xx_[13], uu[3], ll[13];
+  for (int i = 0; i < 13; ++i) { xx_[i] = x[i]; ll[i] = lam[i]; }
+  for (int i = 0; i < 3; ++i) uu[i] = u[i];
+  for (int r = 0; r < 16; ++r) {
+    float o16[16], o5[5], o13[13];
+    R::mcol(r, th, xx_, uu, ll, o16);
+    for (int k = 0; k < 16; ++k) mcol[r * 16 + k] = o16[k];
+    R::mp_row(r, th, xx_, uu, ll, o5);
+    for (int k = 0; k < 5; ++k) mp[r * 5 + k] = o5[k];
+    if (r < 13) {
+      R::xx_row(r, th, xx_, uu, o13);
+      for (int k = 0; k < 13; ++k) xx[r * 13 + k] = o13[k];
+      R::xth_row(r, th, xx_, uu, o5);
+      for (int k = 0; k < 5; ++k) xth[r * 5 + k] = o5[k];
+    }
+  }
+}
 """
 
 
@@ -88,3 +109,29 @@ def test_generated_second_order_terms(shim, golden, name, cls):
         assert np.abs(Mh - ref_Mh).max() / scale(ref_Mh) < 2e-4, b
         assert np.abs(Mp - ref_Mp).max() / scale(ref_Mp) < 2e-4, b
         assert np.abs(ft - fth[b]).max() / scale(fth[b]) < 2e-4, b
+
+
+def test_generated_rocket_pieces(shim, golden):
+    """RocketD2 is built from the reference's build_batched_* tables (rocket.py:
+    541-820), restated in tools/model_sym.py; the oracle's restatement of the same
+    tables is pinned to the reference's get_matrices outputs."""
+    g = golden("models_f64")
+    X, U = g["rocket_x"][:16], g["rocket_u"][:16]
+    D, Dp, Dx, Du, fth, xx, _ = om.Rocket.get_matrices(X, U)
+    th = np.array(om.Rocket.default_params, np.float32)
+    rng = np.random.RandomState(1)
+    scale = lambda a: max(1.0, np.abs(a).max())  # noqa: E731
+    for b in range(X.shape[0]):
+        lam = rng.normal(size=13)
+        x32, u32, l32 = X[b].astype(np.float32), U[b].astype(np.float32), lam.astype(np.float32)
+        outs = [np.zeros(k, np.float32) for k in (256, 80, 169, 65)]
+        shim.Rocket_pieces(*[a.ctypes.data_as(ctypes.c_void_p) for a in (th, x32, u32, l32, *outs)])
+        mcol, mp, xxr, xth = outs[0].reshape(16, 16), outs[1].reshape(16, 5), outs[2].reshape(13, 13), \
+            outs[3].reshape(13, 5)
+        Dtau = np.concatenate([Dx[b], Du[b]], -1)
+        ref_M = np.einsum("i,ijk->jk", lam, Dtau)
+        assert np.abs(mcol.T - ref_M).max() / scale(ref_M) < 2e-4, b
+        ref_Mp = np.einsum("i,ijk->jk", lam, Dp[b])
+        assert np.abs(mp - ref_Mp).max() / scale(ref_Mp) < 2e-4, b
+        assert np.abs(xxr - xx[b]).max() / scale(xx[b]) < 2e-4, b
+        assert np.abs(xth - fth[b]).max() / scale(fth[b]) < 2e-4, b

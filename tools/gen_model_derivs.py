@@ -2,14 +2,23 @@
 """Generate csrc/dilqr_models_gen.h: second-order model terms for the implicit
 (DiLQR) backward, as CSE'd straight-line fp32 device code.
 
-For each model f(x, u; theta) (the same equations as oracle/models.py, i.e. the
-reference env_dx forward without the control clamp) this emits
+For the one-lane-per-problem models (pendulum, cartpole) this emits
   lag_hess(th, x, u, lam, M)    M[j][k]  = sum_i lam_i d D[i][j] / d tau_k      (d x d)
   lag_dparam(th, x, u, lam, Mp) Mp[j][k] = sum_i lam_i D_grad_params[i][j][k]   (d x p)
   f_theta(th, x, u, ft)         ft[i][k] = d f_i / d theta_k                     (n x p)
 where D = df/dtau.  D_grad_params uses the reference's closed forms where they
-differ from the derivative (cartpole.py matrix_2_part_2/3 row 4, see
-oracle/models.py Cartpole.get_matrices), so the kernel reproduces the reference.
+differ from the derivative (cartpole.py matrix_2_part_2/3 row 4).
+
+For the rocket (16 lanes per problem, dilqr_group.h) it emits per-lane pieces,
+built from the reference's build_batched_* tables (rocket.py:541-820) rather
+than from derivatives, since those are what its implicit backward uses:
+  mcol(r, ..., lam, o)   o[k] = sum_i lam_i Dtau[i][k][r]   (column r of M, d)
+  mp_row(j, ..., lam, o) o[k] = sum_i lam_i D_params[i][j][k]                (p)
+  xx_row(r, ..., o)      row r of x_grad_xtm1                                (n)
+  xth_row(r, ..., o)     row r of x_grad_theta = d f_r / d theta             (p)
+
+The equations come from tools/model_sym.py (not from oracle/, which is test
+infrastructure); tests/test_models_gen.py checks the output against the oracle.
 
 Usage: python tools/gen_model_derivs.py   (rewrites the header; commit the result)
 """
@@ -20,8 +29,8 @@ import sympy as sp
 from sympy.printing.c import C99CodePrinter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
-from oracle import models as om  # noqa: E402  (the symbolic equations live there)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import model_sym as ms  # noqa: E402
 
 OUT = os.path.join(ROOT, "differentiable-ilqr_amd", "csrc", "dilqr_models_gen.h")
 
@@ -81,14 +90,22 @@ def emit(name, args_sig, outputs, out_decl, syms):
     return _f32_calls("\n".join(lines))
 
 
-def model_block(M, cls_name, dp_overrides=None):
-    n, m, p = M.n_state, M.n_ctrl, M.n_params
+def unpack_lines(xs, us, ps, lam=None):
+    s = "    " + " ".join(f"[[maybe_unused]] const float {v} = x[{i}];" for i, v in enumerate(xs)) + "\n    " + \
+        " ".join(f"[[maybe_unused]] const float {v} = u[{i}];" for i, v in enumerate(us)) + "\n    " + \
+        " ".join(f"[[maybe_unused]] const float {v} = th[{i}];" for i, v in enumerate(ps))
+    if lam is not None:
+        s += "\n    " + " ".join(f"[[maybe_unused]] const float {v} = lam[{i}];" for i, v in enumerate(lam))
+    return s
+
+
+def model_block(M, cls_name):
+    n, m, p = M.n, M.m, M.p
     d = n + m
-    xs = sp.symbols(f"x0:{n}", real=True)
-    us = sp.symbols(f"u0:{m}", real=True)
-    ps = sp.symbols(f"th0:{p}", real=True)
+    xs, us, ps = ms.symbols(n, m, p)
     lam = sp.symbols(f"lam0:{n}", real=True)
-    f = sp.Matrix(M._sym_next_state(xs, us, ps))
+    dp_overrides = M.dp_overrides()
+    f = sp.Matrix(M.next_state(xs, us, ps))
     tau = list(xs) + list(us)
     D = f.jacobian(tau)
     Dp = [[[sp.diff(D[i, j], ps[k]) for k in range(p)] for j in range(d)] for i in range(n)]
@@ -99,10 +116,8 @@ def model_block(M, cls_name, dp_overrides=None):
     Mp = [[sum(lam[i] * Dp[i][j][k] for i in range(n)) for k in range(p)] for j in range(d)]
     ft = [[sp.diff(f[i], ps[k]) for k in range(p)] for i in range(n)]
 
-    unpack = "    " + " ".join(f"[[maybe_unused]] const float {s} = x[{i}];" for i, s in enumerate(xs)) + "\n    " + \
-        " ".join(f"[[maybe_unused]] const float {s} = u[{i}];" for i, s in enumerate(us)) + "\n    " + \
-        " ".join(f"[[maybe_unused]] const float {s} = th[{i}];" for i, s in enumerate(ps))
-    unpack_l = "\n    " + " ".join(f"[[maybe_unused]] const float {s} = lam[{i}];" for i, s in enumerate(lam))
+    unpack = unpack_lines(xs, us, ps)
+    unpack_l = unpack_lines(xs, us, ps, lam)[len(unpack):]
     sig = f"const float* __restrict__ th, const float (&x)[{n}], const float (&u)[{m}]"
 
     def fn(name, extra_sig, outs, out_decl, with_lam):
@@ -122,43 +137,60 @@ def model_block(M, cls_name, dp_overrides=None):
     return "\n".join(parts)
 
 
-def cartpole_overrides():
-    """The reference's closed forms for D_grad_params[4,3,1], [4,3,2], [4,4,2],
-    [4,5,2] (cartpole.py matrix_2_part_2 / matrix_2_part_3, row 4), restated."""
-    dt = sp.Float(om.Cartpole.dt)
+def emit_switch(name, sig, sel, n_out, cases, unpack):
+    """A per-lane function: switch on `sel`, each case a CSE'd list of outputs
+    (cases: {value: [expr] * n_out}); outputs not written are zero."""
+    lines = [f"  static DEV void {name}(int {sel}, {sig}, float (&o)[{n_out}]) {{", unpack,
+             f"#pragma unroll\n    for (int k = 0; k < {n_out}; ++k) o[k] = 0.f;", f"    switch ({sel}) {{"]
+    for val in sorted(cases):
+        exprs = cases[val]
+        nz = [(k, e) for k, e in enumerate(exprs) if e != 0]
+        if not nz:
+            continue
+        repl, red = sp.cse([e for _, e in nz], symbols=sp.numbered_symbols("s"), optimizations="basic")
+        lines.append(f"      case {val}: {{")
+        lines += [f"        const float {v} = {P.doprint(e)};" for v, e in repl]
+        lines += [f"        o[{k}] = {P.doprint(e)};" for (k, _), e in zip(nz, red)]
+        lines.append("        break;\n      }")
+    lines += ["      default: break;", "    }", "  }"]
+    return _f32_calls("\n".join(lines))
 
-    def common(xs, ps):
-        c, s, w = xs[2], xs[3], xs[4]
-        g, mc, mp, l = ps
-        Mt = mc + mp
-        den = -c ** 2 * mp / Mt + sp.Rational(4, 3)
-        return c, s, w, g, mc, mp, l, Mt, den
 
-    def e431(xs, us, ps):
-        c, s, w, g, mc, mp, l, Mt, den = common(xs, ps)
-        return dt * (-c ** 2 * mp * (-c * w ** 2 * l * mp / Mt + g) / (l * Mt ** 2 * den ** 2)
-                     + c * dt * w ** 2 * mp / (Mt ** 2 * den))
-
-    def e432(xs, us, ps):
-        c, s, w, g, mc, mp, l, Mt, den = common(xs, ps)
-        return dt * (-c ** 2 * mp * (-c * w ** 2 * l * mp / Mt + g) / (l * den ** 2)
-                     + c * dt * w ** 2 * l * mp / Mt ** 2)
-
-    def e442(xs, us, ps):
-        c, s, w, g, mc, mp, l, Mt, den = common(xs, ps)
-        return (-2 * c * dt * w * mp * s * (-c ** 2 * mp / Mt ** 2 + c ** 2 / Mt) / (Mt * den ** 2)
-                + 2 * c * dt * w * mp * s / (Mt ** 2 * den))
-
-    def e452(xs, us, ps):
-        c, s, w, g, mc, mp, l, Mt, den = common(xs, ps)
-        return c * dt / (l * Mt ** 2 * den)
-
-    return {(4, 3, 1): e431, (4, 3, 2): e432, (4, 4, 2): e442, (4, 5, 2): e452}
+def rocket_block():
+    M = ms.Rocket
+    n, m, p = M.n, M.m, M.p
+    d = n + m
+    xs, us, ps = ms.symbols(n, m, p)
+    lam = sp.symbols(f"lam0:{n}", real=True)
+    f = M.next_state(xs, us, ps)
+    xx, Du, Dx, Dp = M.builders(xs, us, ps)
+    # Dtau[i][j][k] = [D_x | D_u][i][j][k]
+    Dtau = {}
+    for (i, j, k), e in Dx.items():
+        Dtau[(i, j, k)] = e
+    for (i, j, a), e in Du.items():
+        Dtau[(i, j, n + a)] = e
+    mcol = {r: [sum((lam[i] * Dtau.get((i, k, r), 0) for i in range(n)), sp.Integer(0)) for k in range(d)]
+            for r in range(d)}
+    mp = {j: [sum((lam[i] * Dp.get((i, j, k), 0) for i in range(n)), sp.Integer(0)) for k in range(p)]
+          for j in range(d)}
+    xxr = {r: [xx.get((r, l), sp.Integer(0)) for l in range(n)] for r in range(n)}
+    xth = {r: [sp.diff(f[r], ps[k]) for k in range(p)] for r in range(n)}
+    sig = f"const float* __restrict__ th, const float (&x)[{n}], const float (&u)[{m}]"
+    sig_l = sig + f", const float (&lam)[{n}]"
+    up, upl = unpack_lines(xs, us, ps), unpack_lines(xs, us, ps, lam)
+    parts = ["struct RocketD2 {",
+             f"  static constexpr int N = {n}, M = {m}, P = {p}, D = {d};",
+             emit_switch("mcol", sig_l, "r", d, mcol, upl),
+             emit_switch("mp_row", sig_l, "j", p, mp, upl),
+             emit_switch("xx_row", sig, "r", n, xxr, up),
+             emit_switch("xth_row", sig, "r", p, xth, up),
+             "};"]
+    return "\n".join(parts)
 
 
 def main():
-    blocks = [model_block(om.Pendulum, "PendulumD2"),
-              model_block(om.Cartpole, "CartpoleD2", cartpole_overrides())]
+    blocks = [model_block(ms.Pendulum, "PendulumD2"), model_block(ms.Cartpole, "CartpoleD2"), rocket_block()]
     hdr = ["// dilqr_models_gen.h — GENERATED by tools/gen_model_derivs.py; do not edit.",
            "// Second-order model terms for the implicit (DiLQR) backward; see the generator.",
            "#pragma once",
