@@ -185,7 +185,20 @@ def secondary_configs(dev):
                             "algorithmic_bytes_per_launch": it_bytes,
                             "frac": it_bytes / (it_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "riccati_sweep": sweep_roofline(n, m, T, B, dev)}
-    del sv, C, c, x0
+    # rocket implicit backward (16-lane groups) at the solution of the timed solves
+    x, u = sv.gather_best()
+    F, _f = ops.linearize(N.MODEL_ROCKET, theta, x, u)
+    K, _k, _ = ops.lqr_backward(C, c, F, n, m, x=x, u=u)
+    g = torch.Generator(device=dev).manual_seed(1)
+    wx = torch.zeros(T, B, n, device=dev)
+    wu = torch.randn(T, B, m, device=dev, generator=g)                 # loss = sum(u * w), SURVEY §8(d)
+    ib = lambda _r: implicit_backward(dx, wx, wu, C, c, None, None, x, u, K, None, None, None)
+    ib(0)
+    ms = _event_ms(stream, ib, 5)
+    out["config3_rocket"]["implicit_backward"] = {
+        "kernel": "k_implicit_backward_group<Rocket> (dC, dc, dtheta)", "avg_ms": ms,
+        "problems_per_s": B / (ms * 1e-3), "batch": B, "T": T, "bounds": "none"}
+    del sv, C, c, x0, x, u, F, K, wx, wu
     # ---- config 4: cartpole T=25 B=65536 with bounds (+-100 reference value, +-10 stress) + implicit backward
     T, B, n, m = 25, 65536, 5, 1
     x0n, qn, pn = make_problems(B)

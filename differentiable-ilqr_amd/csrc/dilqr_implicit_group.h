@@ -1,0 +1,360 @@
+// dilqr_implicit_group.h — the DiLQR implicit backward (k_implicit_backward,
+// dilqr_kernels.hip) for the 16-lanes-per-problem models (rocket, d = 16).
+// Included by dilqr_kernels.hip after dilqr_group.h.
+//
+// Same four passes and the same algebra as the one-lane kernel
+// (oracle/adjoint.py implicit_backward_fast; lqr_step_explicit.py:653-712 with
+// rocket's grad_input, rocket.py:263-323, and its build_batched_* tables,
+// rocket.py:541-820), distributed by rows: lane r owns row r of every d x d or
+// n x p quantity.  The pieces come from the generated RocketD2:
+//   mcol(r)   column r of M_t = sum_i lam_{t+1,i} dD_t[i]/dtau   (so row r of
+//             the modified cost C_t + M_t^T is C_t[r] + mcol(r))
+//   mp_row(r) row r of sum_i lam_{t+1,i} dD_t[i]/dtheta
+//   xx_row(r) row r of the reference's x_grad_xtm1 builder
+//   xth_row(r) row r of dx_{t+1}/dtheta
+// and Model::jac_row(r) (row r of D_t, which is also x_grad_utm1's source).
+// Vectors every lane needs in full (gradx, lam, dlam, y) go through LDS; the
+// Riccati step of the modified problem is group_riccati_step.
+#pragma once
+
+#include "dilqr_group.h"
+
+namespace dilqr {
+
+// per-(t,b) workspace record (floats), written lane-contiguous
+template <class Model> struct ImplicitGroupWs {
+  static constexpr int n = Model::N, m = Model::M, p = Model::P;
+  static constexpr int GX = 0;                 // gradx_t, [p][16] (lane r < n: row r)
+  static constexpr int LAM = GX + p * kG;      // lam_t, [16]
+  static constexpr int KG = LAM + kG;          // [m][16]: K[a][r] at r < n, k[a] at n
+  static constexpr int Y = KG + m * kG;        // y_t, [16]
+  static constexpr int REC = Y + kG;
+};
+
+template <int n, int p>
+struct ImplicitGroupLds {
+  float gx[n][p + 1];                          // gradx_{t-1} (phase A)
+  float vec[kG];                               // lam_{t+1} (B) / y_t (C, D)
+  float dlam[kG];                              // dlam_{t+1} (D)
+};
+
+template <class Model, class D2, int MODE>
+__global__ void __launch_bounds__(64) k_implicit_backward_group(
+    int T, int B, const float* __restrict__ theta, const float* __restrict__ C, const float* __restrict__ c,
+    const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ K,
+    const float* __restrict__ dl_dx, const float* __restrict__ dl_du, Bounds bd, float* __restrict__ ws,
+    float* __restrict__ dC, float* __restrict__ dc, float* __restrict__ dtheta) {
+  constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m;
+  static_assert(d <= kG, "one row per lane");
+  using W = ImplicitGroupWs<Model>;
+  __shared__ GroupLds<n, m> Ls[kGPW];
+  __shared__ ImplicitGroupLds<n, p> Is[kGPW];
+  const int r = threadIdx.x & (kG - 1);
+  const int gp = threadIdx.x / kG;
+  const int b0 = blockIdx.x * kGPW + gp;
+  const bool valid = b0 < B;
+  const int b = valid ? b0 : B - 1;           // a padding group recomputes problem B-1, writes nothing
+  GroupLds<n, m>& L = Ls[gp];
+  ImplicitGroupLds<n, p>& I = Is[gp];
+  Model md;
+  md.load(theta);
+  auto rec = [&](int t) { return ws + ((size_t)t * B + b) * W::REC; };
+  auto active = [&](size_t tb, int a, float ua) -> bool {
+    if (bd.mode == DILQR_BOUNDS_NONE) return false;
+    return fabsf(ua - bound_lo(bd, tb * m + a)) <= 1e-8f || fabsf(ua - bound_hi(bd, tb * m + a)) <= 1e-8f;
+  };
+  auto load_tau = [&](size_t tb, float (&xt)[n], float (&ut)[m]) {   // the group's lanes read the same bytes
+#pragma unroll
+    for (int i = 0; i < n; ++i) xt[i] = x[tb * n + i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) ut[a] = u[tb * m + a];
+  };
+  // ---------------- A: gradx_t, t = 0..T-1 (grad_input, rocket.py:263-323 / cartpole.py:755-769)
+  {
+    float gx[p];
+#pragma unroll
+    for (int k = 0; k < p; ++k) gx[k] = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const size_t tb = (size_t)t * B + b;
+      if (t > 0) {
+        if (r < n) {
+#pragma unroll
+          for (int k = 0; k < p; ++k) I.gx[r][k] = gx[k];
+        }
+        __syncthreads();
+        float xt[n], ut[m];
+        load_tau(tb, xt, ut);
+        float Kq[m][n];                                   // K[t-1] of the reversed stack = K_{T-t}
+        const float* Kp = K + ((size_t)(T - t) * B + b) * m * n;
+#pragma unroll
+        for (int a = 0; a < m; ++a)
+#pragma unroll
+          for (int l = 0; l < n; ++l) Kq[a][l] = Kp[a * n + l];
+        if (r < n) {
+          float xx[n], Dr[d], ft[p];
+          D2::xx_row(r, theta, xt, ut, xx);
+          md.jac_row(r, xt, ut, Dr);
+          D2::xth_row(r, theta, xt, ut, ft);
+          float A[n];
+#pragma unroll
+          for (int l = 0; l < n; ++l) {
+            float s = xx[l];
+#pragma unroll
+            for (int a = 0; a < m; ++a) s += Dr[n + a] * Kq[a][l];
+            A[l] = s;
+          }
+#pragma unroll
+          for (int k = 0; k < p; ++k) {
+            float s = 0.f;
+#pragma unroll
+            for (int l = 0; l < n; ++l) s += A[l] * I.gx[l][k];
+            gx[k] = ft[k] + s;
+          }
+        }
+        __syncthreads();
+      }
+      if (valid && r < n) {
+        float* R0 = rec(t);
+#pragma unroll
+        for (int k = 0; k < p; ++k) R0[W::GX + k * kG + r] = gx[k];
+      }
+    }
+  }
+  // ---------------- B: costates, M_t, Riccati of the C + M^T problem (active set masked)
+  {
+    if (r < n) {
+#pragma unroll
+      for (int kk = 0; kk < GroupLds<n, m>::W; ++kk) L.V[r][kk] = 0.f;
+      L.v[r] = 0.f;
+    }
+    if (r < kG) I.vec[r] = 0.f;
+    float prev_k[m];
+#pragma unroll
+    for (int a = 0; a < m; ++a) prev_k[a] = 0.f;
+    bool have_prev = false;
+    int nqp = 0;
+    __syncthreads();
+    for (int t = T - 1; t >= 0; --t) {
+      const size_t tb = (size_t)t * B + b;
+      float xt[n], ut[m], Crow[d], cr = 0.f, gr = 0.f;
+      load_tau(tb, xt, ut);
+#pragma unroll
+      for (int j = 0; j < d; ++j) Crow[j] = 0.f;
+      if (r < d) {
+        ld(Crow, C + (tb * d + r) * d);
+        cr = c[tb * d + r];
+        gr = r < n ? dl_dx[tb * n + r] : dl_du[tb * m + (r - n)];
+      }
+      float lam1[n];
+#pragma unroll
+      for (int i = 0; i < n; ++i) lam1[i] = I.vec[i];     // lam_{t+1} (0 at t = T-1)
+      float Mc[d];
+      if (t < T - 1) {
+        D2::mcol(r, theta, xt, ut, lam1, Mc);
+        if (r < n) {
+          float Fr[d];
+          md.jac_row(r, xt, ut, Fr);
+#pragma unroll
+          for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < d; ++j) Mc[j] = 0.f;
+        if (r < n) {
+#pragma unroll
+          for (int j = 0; j < d; ++j) L.F[r][j] = 0.f;
+        }
+      }
+      __syncthreads();
+      float Cp[d];
+#pragma unroll
+      for (int j = 0; j < d; ++j) Cp[j] = r < d ? Crow[j] + Mc[j] : 0.f;
+      float zI[m], lb[m], ub[m];
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        zI[a] = active(tb, a, ut[a]) ? 1.f : 0.f;
+        lb[a] = ub[a] = 0.f;
+      }
+      float Kt[m][n], kt[m];
+      group_riccati_step<n, m, MODE>(L, r, Cp, -gr, zI, lb, ub, Kt, kt, prev_k, have_prev, nqp);
+      // lam_t = Cxx x + Cxu u + c_x + F_x^T lam_{t+1}   (lqr_step_explicit.py:305-319)
+      float lam_r = 0.f;
+      if (r < n) {
+        float s = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += Crow[j] * xt[j];
+#pragma unroll
+        for (int a = 0; a < m; ++a) s2 += Crow[n + a] * ut[a];
+#pragma unroll
+        for (int l = 0; l < n; ++l) s3 += L.F[l][r] * lam1[l];
+        lam_r = ((s + s2) + cr) + s3;
+      }
+      if (valid) {
+        float* R0 = rec(t);
+        if (r < n) {
+#pragma unroll
+          for (int a = 0; a < m; ++a) R0[W::KG + a * kG + r] = L.Kk[a][r];
+          R0[W::LAM + r] = lam_r;
+        } else if (r == n) {
+#pragma unroll
+          for (int a = 0; a < m; ++a) R0[W::KG + a * kG + n] = L.Kk[a][GroupLds<n, m>::W];
+        }
+      }
+      __syncthreads();                                     // every lane is done with lam_{t+1}, F, Kk
+      if (r < n) I.vec[r] = lam_r;
+      __syncthreads();
+    }
+  }
+  // ---------------- C: rollout y of the modified problem (linear, alpha = 1)
+  {
+    float yx = 0.f;                                        // lane r < n: y_t[r]
+    for (int t = 0; t < T; ++t) {
+      const size_t tb = (size_t)t * B + b;
+      float* R0 = rec(t);
+      float Kc[m], kt[m], ut[m], xt[n];
+      load_tau(tb, xt, ut);
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        Kc[a] = r < n ? R0[W::KG + a * kG + r] : 0.f;
+        kt[a] = R0[W::KG + a * kG + n];
+      }
+      float yr = r < n ? yx : 0.f;
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        const float s = group_sum(Kc[a] * (r < n ? yx : 0.f));
+        const float ya = active(tb, a, ut[a]) ? 0.f : (s + 0.f) + kt[a];
+        yr = (r == n + a) ? ya : yr;
+      }
+      if (valid && r < d) R0[W::Y + r] = yr;
+      if (t < T - 1) {
+        if (r < d) I.vec[r] = yr;
+        __syncthreads();
+        if (r < n) {
+          float Dr[d];
+          md.jac_row(r, xt, ut, Dr);
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < d; ++j) s += Dr[j] * I.vec[j];
+          yx = s;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  // ---------------- D: w, dlam, dC, dc, dtheta
+  {
+    float acc[p], gx1[p];
+#pragma unroll
+    for (int k = 0; k < p; ++k) acc[k] = gx1[k] = 0.f;
+    if (r < kG) I.dlam[r] = 0.f;
+    __syncthreads();
+    for (int t = T - 1; t >= 0; --t) {
+      const size_t tb = (size_t)t * B + b;
+      const float* R0 = rec(t);
+      float xt[n], ut[m], y[d], Crow[d], gr = 0.f;
+      load_tau(tb, xt, ut);
+#pragma unroll
+      for (int j = 0; j < d; ++j) { y[j] = R0[W::Y + j]; Crow[j] = 0.f; }
+      if (r < d) {
+        ld(Crow, C + (tb * d + r) * d);
+        gr = r < n ? dl_dx[tb * n + r] : dl_du[tb * m + (r - n)];
+      }
+      float gx[p];
+#pragma unroll
+      for (int k = 0; k < p; ++k) gx[k] = r < n ? R0[W::GX + k * kG + r] : 0.f;
+      float tau[d];
+#pragma unroll
+      for (int i = 0; i < n; ++i) tau[i] = xt[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+      float yr = 0.f, taur = 0.f;
+#pragma unroll
+      for (int j = 0; j < d; ++j) { yr = (j == r) ? y[j] : yr; taur = (j == r) ? tau[j] : taur; }
+      // dC_t row r = -0.5 (y_r tau^T + tau_r y^T), dc_t = -y   (lqr_step_explicit.py:296-303)
+      if (valid && r < d) {
+        float dCr[d];
+#pragma unroll
+        for (int j = 0; j < d; ++j) dCr[j] = -0.5f * (yr * tau[j] + taur * y[j]);
+        st(dC + (tb * d + r) * d, dCr);
+        dc[tb * d + r] = -yr;
+      }
+      float dl1[n];
+#pragma unroll
+      for (int i = 0; i < n; ++i) dl1[i] = I.dlam[i];      // dlam_{t+1}
+      float wr = gr, Dtd = 0.f;                            // w_t[r]; (D^T dlam_{t+1})[r]
+      if (t < T - 1) {
+        float lam1[n];
+        const float* R1 = rec(t + 1);
+#pragma unroll
+        for (int i = 0; i < n; ++i) lam1[i] = R1[W::LAM + i];
+        float Mc[d], Mp[p];
+        D2::mcol(r, theta, xt, ut, lam1, Mc);
+        D2::mp_row(r, theta, xt, ut, lam1, Mp);
+        if (r < n) {
+          float Fr[d];
+          md.jac_row(r, xt, ut, Fr);
+#pragma unroll
+          for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
+        }
+        __syncthreads();
+        float z = 0.f;                                     // (M_t^T y_t)[r]
+#pragma unroll
+        for (int j = 0; j < d; ++j) z += Mc[j] * y[j];
+        if (r < d) {
+#pragma unroll
+          for (int i = 0; i < n; ++i) Dtd += L.F[i][r] * dl1[i];
+        }
+        wr = gr - z;
+        // dtheta_t = -(y^T Mp) - (y^T (M_x + M_u Kq)) gradx_t - dlam_{t+1}^T gradx_{t+1}
+        //            + dlam_{t+1}^T (D_x + D_u Kq) gradx_t      (oracle/adjoint.py implicit_backward_fast)
+        float zu[m], du[m];
+#pragma unroll
+        for (int a = 0; a < m; ++a) {
+          zu[a] = __shfl(z, n + a, kG);
+          du[a] = __shfl(Dtd, n + a, kG);
+        }
+        if (r < d) {
+#pragma unroll
+          for (int k = 0; k < p; ++k) acc[k] -= yr * Mp[k];
+        }
+        if (r < n) {
+          const float* Kp = K + ((size_t)(T - 1 - t) * B + b) * m * n;   // K[t] of the reversed stack
+          float sx = z, s2 = Dtd;
+#pragma unroll
+          for (int a = 0; a < m; ++a) {
+            const float Kal = Kp[a * n + r];
+            sx += zu[a] * Kal;
+            s2 += du[a] * Kal;
+          }
+          const float hx = s2 - sx, dlr = I.dlam[r];
+#pragma unroll
+          for (int k = 0; k < p; ++k) acc[k] += hx * gx[k] - dlr * gx1[k];
+        }
+      }
+      // dlam_t = Cxx y_x + Cxu y_u - w_x + F_x^T dlam_{t+1}   (lqr_step_explicit.py:321-335)
+      float nd = 0.f;
+      if (r < n) {
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += Crow[j] * y[j];
+#pragma unroll
+        for (int a = 0; a < m; ++a) s2 += Crow[n + a] * y[n + a];
+        nd = ((s + s2) - wr) + Dtd;
+      }
+#pragma unroll
+      for (int k = 0; k < p; ++k) gx1[k] = gx[k];
+      __syncthreads();
+      if (r < n) I.dlam[r] = nd;
+      __syncthreads();
+    }
+    float dth = 0.f;
+#pragma unroll
+    for (int k = 0; k < p; ++k) {
+      const float s = group_sum(acc[k]);
+      dth = (r == k) ? s : dth;
+    }
+    if (valid && r < p) dtheta[(size_t)b * p + r] = dth;
+  }
+}
+
+}  // namespace dilqr

@@ -20,6 +20,7 @@ DEV float bound_hi(const Bounds& bd, long long idx) { return bd.mode == DILQR_BO
 }  // namespace dilqr
 
 #include "dilqr_group.h"   // 16-lanes-per-problem kernels (rocket-sized d <= 16)
+#include "dilqr_implicit_group.h"   // the implicit backward for those models
 
 namespace dilqr {
 
@@ -2029,6 +2030,7 @@ int dilqr_implicit_ws_floats(int model) {
   switch (model) {
     case DILQR_MODEL_PENDULUM: return ImplicitWs<Pendulum>::REC;
     case DILQR_MODEL_CARTPOLE: return ImplicitWs<Cartpole>::REC;
+    case DILQR_MODEL_ROCKET: return ImplicitGroupWs<Rocket>::REC;
     default: return -1;
   }
 }
@@ -2044,6 +2046,15 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta, con
   if (bad_bounds(bounds)) return DILQR_E_ARG;
   if (B == 0) return 0;
   Bounds bd = mkb(bounds);
+  if (model == DILQR_MODEL_ROCKET) {
+    if (bd.mode == DILQR_BOUNDS_NONE)
+      k_implicit_backward_group<Rocket, gen::RocketD2, GAIN_UNC><<<grid_group(B), 64, 0, S(stream)>>>(
+          T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta);
+    else
+      k_implicit_backward_group<Rocket, gen::RocketD2, GAIN_ZERO_I><<<grid_group(B), 64, 0, S(stream)>>>(
+          T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta);
+    return launched();
+  }
   MODEL_SWITCH_TPP(model, (k_implicit_backward<MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
                           T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta)));
   return launched();

@@ -1,5 +1,6 @@
 """DiLQR implicit backward (lqr_step_explicit.py:653-712) on the HIP path: one
-fused kernel per call (dilqr_implicit_backward_f32)."""
+fused kernel per call (dilqr_implicit_backward_f32): one lane per problem for
+pendulum and cartpole, a 16-lane group per problem for rocket."""
 import torch
 
 from . import _native as N
@@ -11,8 +12,8 @@ def implicit_backward(model, dl_dx, dl_du, C, c, F, f, x, u, K, u_lower, u_upper
     gains in natural time order (the kernel applies the reference's reversed
     stacking).  F, f are not needed: the kernel re-linearises at (x, u)."""
     mid = ops.model_id_of(model)
-    if mid not in (N.MODEL_CARTPOLE, N.MODEL_PENDULUM):
-        raise NotImplementedError("dilqr: implicit backward is implemented for cartpole and pendulum")
+    if mid not in (N.MODEL_CARTPOLE, N.MODEL_PENDULUM, N.MODEL_ROCKET):
+        raise NotImplementedError("dilqr: the implicit backward needs a pendulum, cartpole or rocket model")
     T, B, n = x.shape
     m = u.shape[2]
     d = n + m

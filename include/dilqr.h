@@ -204,7 +204,9 @@ int dilqr_lqr_adjoint_f32(int n, int m, int T, int B, const float* C, const floa
    reference's reversed-stack indexing itself), C, c, theta, dl_dx, dl_du, the
    box bounds (active set |u - bound| <= 1e-8).  Outputs dC [T,B,d,d], dc [T,B,d],
    dtheta [B,p] (per problem; the autograd caller sums over the batch).
-   ws: T*B*dilqr_implicit_ws_floats(model) floats.  Models: pendulum, cartpole. */
+   ws: T*B*dilqr_implicit_ws_floats(model) floats.  Models: pendulum, cartpole (one lane per
+   problem), rocket (16 lanes per problem, rocket.py:263-323 and its builder
+   tables 541-820). */
 int dilqr_implicit_ws_floats(int model);
 int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
                                 const float* C, const float* c, const float* x,

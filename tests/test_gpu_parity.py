@@ -255,7 +255,8 @@ def test_full_size_batch_independence():
 
 # ------------------------------------------------------------------ DiLQR implicit backward
 IMPLICIT = {"cart_unc": ("cartpole", None), "cart_box": ("cartpole", (-5.0, 5.0)),
-            "pend_box": ("pendulum", (-2.0, 2.0))}
+            "pend_box": ("pendulum", (-2.0, 2.0)), "rock_unc": ("rocket", None),
+            "rock_box": ("rocket", (-10.0, 10.0))}
 
 
 @pytest.mark.parametrize("tag", list(IMPLICIT))
@@ -339,6 +340,55 @@ def test_implicit_backward_full_size():
                                        c[:, sl].contiguous(), None, None, x[:, sl].contiguous(),
                                        u[:, sl].contiguous(), K[:, sl].contiguous(), -10.0, 10.0, None)
     assert torch.equal(dth[sl], dth2) and torch.equal(dC[:, sl], dC2)
+
+
+def rocket_x0(B, seed=0):
+    """near-hover initial states, SURVEY.md §8(d) config 3"""
+    rng = np.random.RandomState(seed)
+    r = rng.uniform([0, -4, -2.5], [10, 4, 2.5], (B, 3))
+    v = rng.normal(0, 0.1, (B, 3))
+    q4 = np.array([1., 0, 0, 0]) + 0.05 * rng.normal(size=(B, 4))
+    q4 /= np.linalg.norm(q4, axis=1, keepdims=True)
+    w = rng.normal(0, 0.02, (B, 3))
+    return np.concatenate([r, v, q4, w], 1)
+
+
+@pytest.mark.parametrize("bounds", [None, (-10.0, 10.0)])
+def test_implicit_backward_rocket_full_size(bounds):
+    """Config 3 shape (rocket T=30, B=32768) through the 16-lane implicit kernel:
+    finite gradients, a 64-problem slice gives bit-identical per-problem results,
+    and a small slice matches the oracle's fast algebra run on the same fp32
+    solution (fp64 oracle, 1e-3 of the max magnitude: the GPU works in fp32)."""
+    from dilqr import ops
+    from dilqr.implicit import implicit_backward
+    B, T, n, m = 32768, 30, 13, 3
+    x0 = rocket_x0(B)
+    x, u, _ = run_gpu_mpc(x0, "rocket", T, 10, bounds, 0.0, 10 ** 9, 0.2, 5)
+    dx = dilqr_models()["rocket"]()
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV)
+    c = p.repeat(T, B, 1).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    wx = torch.randn(T, B, n, device=DEV, generator=g)
+    wu = torch.randn(T, B, m, device=DEV, generator=g)
+    lo, hi = bounds if bounds else (None, None)
+    F = ops.linearize(dx.model_id, ops.theta_of(dx, C), x, u)[0]
+    K, _, _ = ops.lqr_backward(C, c, F, n, m, x=x, u=u, u_lower=lo, u_upper=hi)
+    dC, dc, dth = implicit_backward(dx, wx, wu, C, c, None, None, x, u, K, lo, hi, None)
+    assert torch.isfinite(dC).all() and torch.isfinite(dc).all() and torch.isfinite(dth).all()
+    sl = slice(5000, 5064)
+    cut = lambda a: a[:, sl].contiguous()  # noqa: E731
+    dC2, dc2, dth2 = implicit_backward(dx, cut(wx), cut(wu), cut(C), cut(c), None, None, cut(x), cut(u), cut(K),
+                                       lo, hi, None)
+    assert torch.equal(dth[sl], dth2) and torch.equal(dC[:, sl], dC2) and torch.equal(dc[:, sl], dc2)
+    so = slice(7, 11)
+    f64 = lambda a: cpu(a[:, so]).astype(np.float64)  # noqa: E731
+    K_rev = f64(K)[::-1].copy()
+    rdC, rdc, rdth = oadj.implicit_backward_fast(omodels.Rocket, f64(wx), f64(wu), f64(C), f64(c), f64(F), None,
+                                                 f64(x), f64(u), K_rev, lo, hi)
+    assert relerr(cpu(dth[so]), rdth) < 1e-3
+    assert relerr(cpu(dc[:, so]), rdc) < 1e-3
+    assert relerr(cpu(dC[:, so]), rdC) < 1e-3
 
 
 # ------------------------------------------------------------------ 16-lanes-per-problem kernels (rocket)
