@@ -550,10 +550,13 @@ DEV void st_traj(float* __restrict__ p, const float (&r)[K], size_t t, int B, in
 }
 
 // Where the fused kernels read the stage cost from: the caller's C [T,B,d,d] and
-// c [T,B,d], or the solve's packed copy (symmetric C: upper triangle row-major,
-// then c, padded to a multiple of 4 floats per (t,b), float4-column layout),
-// written by the solve's iteration 0.  Both fill the same full registers, so
-// the arithmetic is identical.
+// c [T,B,d], or the solve's packed copy of a symmetric C, written by the solve's
+// iteration 0: per (t,b) the diagonal of C, then c, then the strict upper
+// triangle row-major (float4-column layout).  A problem whose C_t are all
+// diagonal (every off-diagonal entry +0.0 bit for bit — the reference's own
+// callers pass diag(q), il_env.py:159-162) reads only the leading 2d floats and
+// holds literal zeros off the diagonal.  All variants fill the same full
+// registers with the same values, so the arithmetic is identical.
 template <int d>
 struct CostFull {
   const float* __restrict__ C;
@@ -566,22 +569,69 @@ struct CostFull {
 
 template <int d>
 constexpr int packed_cost_floats() { return d * (d + 1) / 2 + d; }
+// the diagonal-only read needs the leading 2d floats to be whole float4 planes
+template <int d>
+constexpr bool packed_diag_ok() { return (2 * d) % 4 == 0; }
+
+// cost_sym[b] flags written by iteration 0
+constexpr unsigned char kCostSym = 1, kCostDiag = 2;
 
 template <int d>
+DEV void pack_cost(const float (&C)[d][d], const float (&c)[d], float (&buf)[packed_cost_floats<d>()], bool& sym,
+                   bool& diag) {
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < d; ++i) buf[k++] = C[i][i];
+#pragma unroll
+  for (int i = 0; i < d; ++i) buf[k++] = c[i];
+#pragma unroll
+  for (int i = 0; i < d; ++i)
+#pragma unroll
+    for (int j = i + 1; j < d; ++j) {
+      sym &= __float_as_uint(C[i][j]) == __float_as_uint(C[j][i]);
+      diag &= __float_as_uint(C[i][j]) == 0u && __float_as_uint(C[j][i]) == 0u;
+      buf[k++] = C[i][j];
+    }
+}
+
+template <int d, bool DIAG = false>
 struct CostPacked {
   const float* __restrict__ P;
   int T;
   DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t, int B, int b) const {
     constexpr int PK = packed_cost_floats<d>();
-    float buf[PK];
-    SoaRec<PK>::load(buf, P, T, t, B, b);
-    int k = 0;
+    if constexpr (DIAG) {
+      static_assert(packed_diag_ok<d>(), "diagonal read needs whole float4 planes");
+      constexpr int Q4 = SoaRec<PK>::Q4;
+      const float4* q = reinterpret_cast<const float4*>(P);
+      float buf[2 * d];
 #pragma unroll
-    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < 2 * d / 4; ++j) {
+        float4 v = q[(t * Q4 + j) * B + b];
+        buf[4 * j] = v.x; buf[4 * j + 1] = v.y; buf[4 * j + 2] = v.z; buf[4 * j + 3] = v.w;
+      }
+      const float z = 0.f;
 #pragma unroll
-      for (int j = i; j < d; ++j) { Cr[i][j] = buf[k]; Cr[j][i] = buf[k]; ++k; }
+      for (int i = 0; i < d; ++i) {
 #pragma unroll
-    for (int i = 0; i < d; ++i) cr[i] = buf[k++];
+        for (int j = 0; j < d; ++j) Cr[i][j] = z;
+        Cr[i][i] = buf[i];
+        cr[i] = buf[d + i];
+      }
+    } else {
+      float buf[PK];
+      SoaRec<PK>::load(buf, P, T, t, B, b);
+      int k = 2 * d;
+#pragma unroll
+      for (int i = 0; i < d; ++i) {
+        Cr[i][i] = buf[i];
+        cr[i] = buf[d + i];
+      }
+#pragma unroll
+      for (int i = 0; i < d; ++i)
+#pragma unroll
+        for (int j = i + 1; j < d; ++j) { Cr[i][j] = buf[k]; Cr[j][i] = buf[k]; ++k; }
+    }
   }
 };
 
@@ -634,8 +684,10 @@ struct FwdIn {
 };
 
 // x, u (current trajectory) and the candidate outputs in layout SOA; the gain
-// records in ws and the packed cost are always float4-column.
-template <class Model, int BM, bool SOA, class CostT>
+// records in ws and the packed cost are always float4-column.  ROLLOUT: x is a
+// rollout of the model under u (the MPC slots are), so x_{t+1} = forward(x_t,
+// u_t) bit for bit and models with kJacFromNext take part of the Jacobian from it.
+template <class Model, int BM, bool SOA, bool ROLLOUT, class CostT>
 DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
                      float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
@@ -650,7 +702,10 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
   {
     RiccatiState<n, m> rs;
     rs.init();
-    bool sym = true;
+    bool sym = true, diag = true;
+    float xn[n];                                        // x_{t+1} (ROLLOUT)
+#pragma unroll
+    for (int i = 0; i < n; ++i) xn[i] = 0.f;
     SweepIn<n, m, SOA, BM> cur, nxt;
     cur.load(cs, x, u, bd, T - 1, B, b);
     for (int t = T - 1; t >= 0; --t) {
@@ -663,16 +718,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       if (pack_out) {                                   // first iteration: build the packed copy
         constexpr int PK = packed_cost_floats<d>();
         float buf[PK];
-        int kk = 0;
-#pragma unroll
-        for (int i = 0; i < d; ++i)
-#pragma unroll
-          for (int j = i; j < d; ++j) {
-            sym &= __float_as_uint(cur.C[i][j]) == __float_as_uint(cur.C[j][i]);
-            buf[kk++] = cur.C[i][j];
-          }
-#pragma unroll
-        for (int i = 0; i < d; ++i) buf[kk++] = cur.c[i];
+        pack_cost(cur.C, cur.c, buf, sym, diag);
         SoaRec<PK>::store(pack_out, buf, T, t, B, b);
       }
       float obj = quad_cost(cur.C, cur.c, tau, Ctau);
@@ -680,7 +726,8 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + cur.c[i];
       float Ft[n][d];
       if (t < T - 1) {
-        md.jacobian(cur.x, cur.u, Ft);
+        if constexpr (ROLLOUT && Model::kJacFromNext) md.jacobian_next(cur.x, cur.u, xn, Ft);
+        else md.jacobian(cur.x, cur.u, Ft);
       } else {
 #pragma unroll
         for (int i = 0; i < n; ++i)
@@ -707,9 +754,11 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       }
       SoaRec<GREC>::store(ws, g, T, t, B, b);
       old_cost += obj;          // summed over t = T-1..0 (the reference's torch sum has its own order)
+#pragma unroll
+      for (int i = 0; i < n; ++i) xn[i] = cur.x[i];
       cur = nxt;
     }
-    if (sym_out) sym_out[b] = sym ? 1 : 0;
+    if (sym_out) sym_out[b] = sym ? (diag && packed_diag_ok<d>() ? kCostSym | kCostDiag : kCostSym) : 0;
   }
   // ---------------- forward: the line search (lqr_step_explicit.py:166-263).
   // Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
@@ -826,7 +875,7 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
   // over (x_out, u_out) when it wins
   float* xb = ws + (size_t)T * B * GREC;
   float* ub = xb + (size_t)T * B * n;
-  const int win = ilqr_problem<Model, BM, false>(T, B, b, md, x_init, CostFull<n + m>{C, c}, nullptr, nullptr, x, u,
+  const int win = ilqr_problem<Model, BM, false, false>(T, B, b, md, x_init, CostFull<n + m>{C, c}, nullptr, nullptr, x, u,
                                                    bd, decay,
                                             max_ls, ws,
                                             x_out, u_out, xb, ub, du_sq, cost, alpha);
@@ -886,14 +935,24 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   int win;
   // the solve's packed symmetric cost: built by iteration 0's sweep (which reads
   // C, c), used from iteration 1 on by every problem whose C_t are all bitwise
-  // symmetric (per-lane flag; a wave normally takes one side of the branch)
+  // symmetric, reading only diag(C_t) and c_t when they are all diagonal too
+  // (per-lane flags; a wave normally takes one side of the branch)
   const CostFull<n + m> full{C, c};
-  if (!first && S.Cpk && S.cost_sym[b])
-    win = ilqr_problem<Model, BM, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
+  const unsigned char pk = (!first && S.Cpk) ? S.cost_sym[b] : 0;
+  if (pk & kCostDiag) {                  // set by iteration 0 only when packed_diag_ok
+    if constexpr (packed_diag_ok<n + m>())
+      win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr, nullptr,
+                                          S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws,
+                                          S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm,
+                                          S.du_sq, cost, alpha);
+    else
+      __builtin_unreachable();
+  } else if (pk & kCostSym)
+    win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
                                     S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn,
                                     S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost, alpha);
   else
-    win = ilqr_problem<Model, BM, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
+    win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
                                     first && S.Cpk ? S.cost_sym : nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd,
                                     decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
                                     S.Us + sb * TBm, S.du_sq, cost, alpha);

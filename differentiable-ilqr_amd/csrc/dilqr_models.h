@@ -18,6 +18,11 @@ struct Pendulum {
   float g, m, l;
   DEV void load(const float* __restrict__ th) { g = th[0]; m = th[1]; l = th[2]; }
 
+  static constexpr bool kJacFromNext = false;   // its Jacobian angle uses the unclamped u
+  DEV void jacobian_next(const float (&x)[N], const float (&u)[M], const float (&)[N], float (&D)[N][N + M]) const {
+    jacobian(x, u, D);
+  }
+
   struct FSparsity {      // pendulum.py:448-474: row 2 has a structural zero at cos
     static constexpr bool nz(int i, int j) { return !(i == 2 && j == 0); }
   };
@@ -91,8 +96,30 @@ struct Cartpole {
     o[4] = dth + DT * th_acc;
   }
 
+  // the angle forward() integrates to, rounded as forward() and the reference's
+  // dt * dth + atan2(sin, cos) (cartpole.py:825-834) round it: no contraction
+  DEV static float next_angle(float c, float s, float w) {
+#pragma clang fp contract(off)
+    return atan2f(s, c) + DT * w;
+  }
+
   // cartpole.py:790-839 (closed form of the same derivative)
   DEV void jacobian(const float (&s_)[N], const float (&u)[M], float (&D)[N][N + M]) const {
+    const float th2 = next_angle(s_[2], s_[3], s_[4]);
+    jacobian_sc(s_, u, cosf(th2), sinf(th2), D);
+  }
+
+  // The Jacobian's cos/sin of the integrated angle are exactly components 2 and
+  // 3 of forward(x, u) (same angle, same rounding, independent of u), so along a
+  // rollout the fused sweep takes them from x_{t+1} instead of recomputing
+  // atan2, sin and cos.
+  static constexpr bool kJacFromNext = true;
+  DEV void jacobian_next(const float (&s_)[N], const float (&u)[M], const float (&xn)[N],
+                         float (&D)[N][N + M]) const {
+    jacobian_sc(s_, u, xn[2], xn[3], D);
+  }
+
+  DEV void jacobian_sc(const float (&s_)[N], const float (&u)[M], float cs, float sn, float (&D)[N][N + M]) const {
     float c = s_[2], s = s_[3], w = s_[4], uu = u[0];
     float Mt = mc + mp, iM = 1.0f / Mt;
     float pml = mp * l;
@@ -113,8 +140,6 @@ struct Cartpole {
     float xa_w = A_w * iM - k * tha_w * c;
     float xa_u = iM - k * tha_u * c;
     float ir2 = 1.0f / (c * c + s * s);
-    float th2 = DT * w + atan2f(s, c);
-    float sn = sinf(th2), cs = cosf(th2);
     D[0][0] = 1.f; D[0][1] = DT;  D[0][2] = 0.f;            D[0][3] = 0.f;            D[0][4] = 0.f;            D[0][5] = 0.f;
     D[1][0] = 0.f; D[1][1] = 1.f; D[1][2] = DT * xa_c;      D[1][3] = DT * xa_s;      D[1][4] = DT * xa_w;      D[1][5] = DT * xa_u;
     D[2][0] = 0.f; D[2][1] = 0.f; D[2][2] = s * sn * ir2;   D[2][3] = -c * sn * ir2;  D[2][4] = -DT * sn;       D[2][5] = 0.f;

@@ -130,7 +130,7 @@ def ilqr_ws_floats(n, m):
 class MPCWorkspace:
     """Device buffers of one MPC solve (reused across iterations)."""
 
-    def __init__(self, T, B, n, m, device):
+    def __init__(self, T, B, n, m, device, packed_cost=True):
         dev = device
         self.xa = torch.empty(T, B, n, device=dev)
         self.ua = torch.empty(T, B, m, device=dev)
@@ -153,7 +153,7 @@ class MPCSolve:
     slots per problem (current, best, two line-search candidates), per-problem
     best bookkeeping, the loop control block."""
 
-    def __init__(self, T, B, n, m, device):
+    def __init__(self, T, B, n, m, device, packed_cost=True):
         dev = device
         self.T, self.B, self.n, self.m = T, B, n, m
         # slots are component-major [4,T,n,B] for the thread-per-problem models
@@ -176,7 +176,7 @@ class MPCSolve:
         self.counter = torch.zeros(16 + 4 * ((B + 63) // 64), dtype=torch.int32, device=dev)
         # packed symmetric-cost copy for the thread-per-problem fused kernels (d <= 8)
         pk = N.lib().dilqr_mpc_packed_cost_floats(n, m)
-        self.Cpk = torch.empty(T * B * pk, device=dev) if n + m <= 8 else None
+        self.Cpk = torch.empty(T * B * pk, device=dev) if n + m <= 8 and packed_cost else None
         self.cost_sym = torch.zeros(B, dtype=torch.uint8, device=dev) if self.Cpk is not None else None
         self.state = N.MpcState(*[t.data_ptr() if t is not None else None for t in (
             self.Xs, self.Us, self.slot, self.best_cost, self.best_du, self.improved, self.cost, self.alpha,

@@ -224,12 +224,14 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
    ws: T*B*ceil4(m*n+m+1) floats.  done_counter: the stop rule's sync area of
    16 + 4*ceil(B/64) uints.  ctrl: two dilqr_mpc_ctrl (ping-pong, zeroed by begin).
    Cpk (nullable) + cost_sym [B] (uint8): the solve's packed copy of a
-   symmetric cost, T*B*dilqr_mpc_packed_cost_floats(n,m) floats (upper triangle
-   of C_t,b row-major, then c_t,b; component-major).  Iteration 0 (first != 0)
-   reads C, c and writes the copy and, per problem, whether all its C_t are
-   bitwise symmetric; later iterations of those problems read the copy (27
-   instead of 42 floats per step at d=6; identical arithmetic).  The cost passed
-   to the iterations of one solve must not change. */
+   symmetric cost, T*B*dilqr_mpc_packed_cost_floats(n,m) floats (diag of C_t,b,
+   then c_t,b, then the strict upper triangle row-major; component-major).
+   Iteration 0 (first != 0) reads C, c and writes the copy and, per problem,
+   flags: bit 0 all its C_t bitwise symmetric, bit 1 all off-diagonals +0.0 too.
+   Later iterations of flagged problems read the copy: 27 instead of 42 floats
+   per step at d=6, or 12 for a diagonal cost (diag(q), the reference's own
+   callers, il_env.py:159-162); identical arithmetic.  The cost passed to the
+   iterations of one solve must not change. */
 typedef struct dilqr_mpc_state {
   float* Xs; float* Us; unsigned char* slot; float* best_cost; float* best_du;
   int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;

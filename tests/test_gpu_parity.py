@@ -185,6 +185,52 @@ def test_fused_iteration_equals_unfused(golden, name):
 
 
 # ------------------------------------------------------------------ classic adjoint
+@pytest.mark.parametrize("mname", ["pendulum", "cartpole"])
+def test_packed_cost_paths_bit_identical(mname):
+    """The solve's packed cost copy (diagonal / symmetric / none, chosen per
+    problem by iteration 0) changes only what is read, never the arithmetic: a
+    batch mixing diagonal, dense symmetric and asymmetric C gives bit-identical
+    trajectories and costs with and without the packed copy."""
+    from dilqr import _native as N
+    from dilqr import ops
+    dx = dilqr_models()[mname]()
+    n, m, T, B = dx.n_state, dx.n_ctrl, 12, 256
+    d = n + m
+    g = torch.Generator().manual_seed(3)
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1)
+    L = torch.randn(T, B // 2, d, d, generator=g) * (0.3 / d ** 0.5)
+    C[:, B // 2:] = C[:, B // 2:] + L @ L.transpose(-1, -2)                       # dense symmetric
+    C[:, 3 * B // 4:, 0, 1] += 1e-3                                               # asymmetric
+    c = p.repeat(T, B, 1) + 0.01 * torch.randn(T, B, d, generator=g)
+    C, c = C.to(DEV).contiguous(), c.to(DEV).contiguous()
+    rng = np.random.RandomState(0)
+    if mname == "pendulum":
+        th = rng.uniform(-np.pi / 2, np.pi / 2, B)
+        x0 = np.stack([np.cos(th), np.sin(th), rng.uniform(-1, 1, B)], 1)
+    else:
+        th = rng.uniform(-np.pi, np.pi, B)
+        x0 = np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                       rng.uniform(-1, 1, B)], 1)
+    x0 = gpu(x0)
+    theta = ops.theta_of(dx, x0)
+    nb, _ = N.make_bounds(None, None)
+    out = []
+    for packed in (True, False):
+        sv = ops.MPCSolve(T, B, n, m, DEV, packed_cost=packed)
+        sv.begin(dx.model_id, theta, x0)
+        for i in range(6):
+            sv.iterate(dx.model_id, theta, x0, C, c, nb, 0.5, 4, i, 1e-4, 0.0, 10 ** 9)
+        x, u = sv.gather_best()
+        out.append((x, u, sv.best_cost.clone()))
+        if packed:
+            flags = cpu(sv.cost_sym)
+            assert (flags[:B // 2] == 3).all() and (flags[B // 2:3 * B // 4] == 1).all()
+            assert (flags[3 * B // 4:] == 0).all()
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("tag,bounds", [("m1", None), ("m3", None), ("m1box", (-0.5, 0.5)),
                                         ("m3box", (-0.5, 0.5))])
 def test_classic_adjoint_vs_golden(golden, tag, bounds):

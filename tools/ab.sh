@@ -1,13 +1,17 @@
 #!/usr/bin/env bash
-# A/B timing of two prebuilt libdilqr.so variants on the same box (ab/libdilqr_{A,B}.so),
-# alternating, bench --kernels-only.  Usage: bash tools/ab.sh [rounds]
+# A/B timing of prebuilt libdilqr.so variants on the same box (ab/libdilqr_<V>.so,
+# every variant present), alternating, bench --kernels-only by default.
+# Usage: bash tools/ab.sh [rounds]; AB_CMD overrides the timed command.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 L=differentiable-ilqr_amd/dilqr/libdilqr.so
+cp $L ab/.inplace.so
 for r in $(seq ${1:-3}); do
-  for v in A B; do
-    cp ab/libdilqr_$v.so $L
+  for f in ab/libdilqr_*.so; do
+    v=${f#ab/libdilqr_}; v=${v%.so}
+    cp $f $L
     out=$(timeout -k 10 300 python ${AB_CMD:-bench.py --kernels-only ${BENCH_ARGS:-}} | tail -1) || exit 1
     echo "$v $out"
   done
 done
+cp ab/.inplace.so $L
