@@ -326,7 +326,7 @@ struct RiccatiState {
 
   // mode GAIN_ZERO_I uses zI[M] (1 = active); GAIN_BOX uses lb/ub [M] (already
   // lower-u_t / upper-u_t, lqr_step_explicit.py:132-133).
-  template <int MODE, class FS = DenseF>
+  template <int MODE, class FS = DenseF, bool DIAG = false>
   DEV void step(const float (&C)[D][D], const float (&cb)[D], const float (&F)[N][D],
                 const float (&zI)[M], const float (&lb)[M], const float (&ub)[M],
                 float (&K)[M][N], float (&k)[M]) {
@@ -351,7 +351,7 @@ struct RiccatiState {
 #pragma unroll
         for (int kk = 0; kk < N; ++kk)
           if (FS::nz(kk, j)) s += P[i][kk] * F[kk][j];
-        Q[i][j] = C[i][j] + s;
+        Q[i][j] = (DIAG && i != j) ? s : C[i][j] + s;     // DIAG: C[i][j] is +0.0
       }
       float s = 0.f;
 #pragma unroll
@@ -487,15 +487,22 @@ struct RiccatiState {
 // 0.5*bquad(tau, C) + bdot(tau, c)  (util.py:130-153 / lqr_step_explicit.py:234);
 // also returns C tau (for c_back = C tau + c), and forms the quadratic term as
 // tau . (C tau) so the product is computed once.
-template <int D>
+// DIAG: every off-diagonal C entry is +0.0 (the packed diagonal cost), so the
+// row sums reduce to their one nonzero term — the same value the full sum
+// rounds to (adding exact zeros changes nothing but the sign of a zero).
+template <int D, bool DIAG = false>
 DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D],
                     float (&Ctau)[D]) {
 #pragma unroll
   for (int i = 0; i < D; ++i) {
-    float s = 0.f;
+    if constexpr (DIAG) {
+      Ctau[i] = C[i][i] * tau[i];
+    } else {
+      float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < D; ++j) s += C[i][j] * tau[j];
-    Ctau[i] = s;
+      for (int j = 0; j < D; ++j) s += C[i][j] * tau[j];
+      Ctau[i] = s;
+    }
   }
   float quad = 0.f, lin = 0.f;
 #pragma unroll
@@ -506,14 +513,18 @@ DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&t
   return 0.5f * quad + lin;
 }
 
-template <int D>
+template <int D, bool DIAG = false>
 DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D]) {
   float quad = 0.f;
 #pragma unroll
   for (int j = 0; j < D; ++j) {
     float r = 0.f;
+    if constexpr (DIAG) {
+      r = tau[j] * C[j][j];
+    } else {
 #pragma unroll
-    for (int i = 0; i < D; ++i) r += tau[i] * C[i][j];
+      for (int i = 0; i < D; ++i) r += tau[i] * C[i][j];
+    }
     quad += r * tau[j];
   }
   float lin = 0.f;

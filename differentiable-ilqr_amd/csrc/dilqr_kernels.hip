@@ -559,6 +559,7 @@ DEV void st_traj(float* __restrict__ p, const float (&r)[K], size_t t, int B, in
 // registers with the same values, so the arithmetic is identical.
 template <int d>
 struct CostFull {
+  static constexpr bool kDiag = false;
   const float* __restrict__ C;
   const float* __restrict__ c;
   DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t, int B, int b) const {
@@ -596,6 +597,7 @@ DEV void pack_cost(const float (&C)[d][d], const float (&c)[d], float (&buf)[pac
 
 template <int d, bool DIAG = false>
 struct CostPacked {
+  static constexpr bool kDiag = DIAG;
   const float* __restrict__ P;
   int T;
   DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t, int B, int b) const {
@@ -721,7 +723,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
         pack_cost(cur.C, cur.c, buf, sym, diag);
         SoaRec<PK>::store(pack_out, buf, T, t, B, b);
       }
-      float obj = quad_cost(cur.C, cur.c, tau, Ctau);
+      float obj = quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau, Ctau);
 #pragma unroll
       for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + cur.c[i];
       float Ft[n][d];
@@ -744,7 +746,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
         }
       }
       float Kt[m][n], kt[m];
-      rs.template step<MODE, typename Model::FSparsity>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
+      rs.template step<MODE, typename Model::FSparsity, CostT::kDiag>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
       float g[GREC];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
@@ -817,13 +819,13 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       for (int i = 0; i < n; ++i) tau[i] = xA[i];
 #pragma unroll
       for (int a = 0; a < m; ++a) tau[n + a] = nuA[a];
-      cA += quad_cost(cur.C, cur.c, tau);
+      cA += quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau);
       if (twoB) {
 #pragma unroll
         for (int i = 0; i < n; ++i) tau[i] = xB[i];
 #pragma unroll
         for (int a = 0; a < m; ++a) tau[n + a] = nuB[a];
-        cB += quad_cost(cur.C, cur.c, tau);
+        cB += quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau);
       }
       if (t < T - 1) {
         float xnext[n];
