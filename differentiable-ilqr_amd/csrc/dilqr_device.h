@@ -21,6 +21,10 @@
 
 namespace dilqr {
 
+// two floats in a VGPR pair: arithmetic on it compiles to the packed fp32 VALU
+// ops (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32), two FMAs per lane per issue
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 // ------------------------------------------------------------------ loads/stores
 // Vectorised load/store of one lane's contiguous record of K floats.  Record
 // offsets are multiples of K floats and the base is 16-byte aligned (checked on

@@ -18,14 +18,34 @@ namespace dilqr {
 
 constexpr int kG = 16;          // lanes per problem
 constexpr int kGPW = 64 / kG;   // problems per wave (= per workgroup)
+// Occupancy floor of the implicit group kernel (waves per SIMD, i.e. at most
+// 512/N VGPRs): left alone the compiler gives it 185 VGPRs = 2 waves per SIMD;
+// 3 measured 2.38 ms vs 2.43 at config 3, while 4 spills (4.4 ms).  The fused
+// iteration is fastest without a floor (175 VGPRs).
+#ifndef DILQR_GROUP_WAVES
+#define DILQR_GROUP_WAVES 3
+#endif
+constexpr int kGroupWavesPerSimd = DILQR_GROUP_WAVES;
 
 struct GroupNoModel {           // LinDx dynamics (F, f given)
   DEV void load(const float*) {}
 };
 
+// Sum over the 16 lanes of a group in four DPP adds (no LDS crossbar, unlike
+// __shfl_xor's ds_bpermute): lane^1 and lane^2 within each quad (quad_perm),
+// then the other quad of the half-row (row_half_mirror: lane i <-> 7-i) and the
+// other half of the row (row_mirror: i <-> 15-i).  Every step adds two partial
+// sums that their two lanes hold in swapped order, so all 16 lanes end with the
+// bitwise-identical total (group-uniform decisions depend on that).
+template <int CTRL>
+DEV float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 DEV float group_sum(float v) {
-#pragma unroll
-  for (int off = kG / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kG);
+  v += dpp_mov<0xB1>(v);      // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);      // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);     // row_half_mirror
+  v += dpp_mov<0x140>(v);     // row_mirror
   return v;
 }
 
@@ -106,31 +126,43 @@ DEV void group_riccati_step(GroupLds<n, m>& L, int r, const float (&Crow)[n + m]
                             const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&K)[m][n],
                             float (&k)[m], float (&prev_k)[m], bool& have_prev, int& n_qp) {
   constexpr int d = n + m;
+  constexpr int n2 = (n + 1) / 2, d2 = (d + 1) / 2;   // column pairs (the pad columns of V and F are 0)
+  static_assert(2 * d2 <= GroupLds<n, m>::W, "pairs stay inside the padded rows");
   const bool row = r < d;
-  // P row r = F[:, r]^T V ; q_r = cb_r + F[:, r] . v
-  float Fcol[n], P[n];
+  // P row r = F[:, r]^T V ; q_r = cb_r + F[:, r] . v.  The dense products run
+  // on column pairs (v_pk_fma_f32: two FMAs per lane per instruction); each
+  // element still accumulates in the same order with one fma per term, so the
+  // rounding is that of the scalar loop.
+  float Fcol[n];
 #pragma unroll
   for (int l = 0; l < n; ++l) Fcol[l] = row ? L.F[l][r] : 0.f;
+  f2 P2[n2];
 #pragma unroll
-  for (int kk = 0; kk < n; ++kk) P[kk] = 0.f;
+  for (int i = 0; i < n2; ++i) P2[i] = f2{0.f, 0.f};
 #pragma unroll
   for (int l = 0; l < n; ++l) {
+    const f2* Vl = reinterpret_cast<const f2*>(&L.V[l][0]);
 #pragma unroll
-    for (int kk = 0; kk < n; ++kk) P[kk] += Fcol[l] * L.V[l][kk];
+    for (int i = 0; i < n2; ++i) P2[i] = P2[i] + Fcol[l] * Vl[i];
   }
   float qr = 0.f;
 #pragma unroll
   for (int l = 0; l < n; ++l) qr += Fcol[l] * L.v[l];
   qr = cb_r + qr;
   // Q row r = C row r + P row r F
+  f2 S2[d2];
+#pragma unroll
+  for (int i = 0; i < d2; ++i) S2[i] = f2{0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < n; ++kk) {
+    const f2* Fk = reinterpret_cast<const f2*>(&L.F[kk][0]);
+    const float p = (kk & 1) ? P2[kk / 2].y : P2[kk / 2].x;
+#pragma unroll
+    for (int i = 0; i < d2; ++i) S2[i] = S2[i] + p * Fk[i];
+  }
   float Q[d];
 #pragma unroll
-  for (int j = 0; j < d; ++j) {
-    float s = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < n; ++kk) s += P[kk] * L.F[kk][j];
-    Q[j] = Crow[j] + s;
-  }
+  for (int j = 0; j < d; ++j) Q[j] = Crow[j] + ((j & 1) ? S2[j / 2].y : S2[j / 2].x);
   if (r >= n && r < d) {
 #pragma unroll
     for (int j = 0; j < d; ++j) L.Qu[r - n][j] = Q[j];
@@ -162,11 +194,6 @@ DEV void group_riccati_step(GroupLds<n, m>& L, int r, const float (&Crow)[n + m]
     for (int jj = 0; jj < n; ++jj) K[a][jj] = L.Kk[a][jj];
     k[a] = L.Kk[a][GroupLds<n, m>::W];
   }
-  float Qux[m][n];
-#pragma unroll
-  for (int a = 0; a < m; ++a)
-#pragma unroll
-    for (int jj = 0; jj < n; ++jj) Qux[a][jj] = L.Qu[a][jj];
   if (r < n) {
     float Kc[m];
 #pragma unroll
@@ -179,18 +206,25 @@ DEV void group_riccati_step(GroupLds<n, m>& L, int r, const float (&Crow)[n + m]
       for (int a = 0; a < m; ++a) s += Kc[a] * Quu[a][b];
       KcQuu[b] = s;
     }
-    float Vr[n];
+    // V row r on column pairs, K and Q_ux pairs straight from LDS (the pad
+    // column n of the last pair is computed and dropped)
+    f2 V2[n2];
 #pragma unroll
-    for (int kk = 0; kk < n; ++kk) {
-      float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (int i = 0; i < n2; ++i) {
+      f2 s1 = f2{0.f, 0.f}, s2 = f2{0.f, 0.f}, s3 = f2{0.f, 0.f};
 #pragma unroll
       for (int a = 0; a < m; ++a) {
-        s1 += Q[n + a] * K[a][kk];
-        s2 += Kc[a] * Qux[a][kk];
-        s3 += KcQuu[a] * K[a][kk];
+        const f2 Ka = reinterpret_cast<const f2*>(&L.Kk[a][0])[i];
+        const f2 Qa = reinterpret_cast<const f2*>(&L.Qu[a][0])[i];
+        s1 = s1 + Q[n + a] * Ka;
+        s2 = s2 + Kc[a] * Qa;
+        s3 = s3 + KcQuu[a] * Ka;
       }
-      Vr[kk] = ((Q[kk] + s1) + s2) + s3;
+      V2[i] = ((f2{Q[2 * i], Q[2 * i + 1]} + s1) + s2) + s3;
     }
+    float Vr[n];
+#pragma unroll
+    for (int kk = 0; kk < n; ++kk) Vr[kk] = (kk & 1) ? V2[kk / 2].y : V2[kk / 2].x;
     float s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
     for (int a = 0; a < m; ++a) {

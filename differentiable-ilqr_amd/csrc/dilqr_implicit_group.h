@@ -39,7 +39,7 @@ struct ImplicitGroupLds {
 };
 
 template <class Model, class D2, int MODE>
-__global__ void __launch_bounds__(64) k_implicit_backward_group(
+__global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_group(
     int T, int B, const float* __restrict__ theta, const float* __restrict__ C, const float* __restrict__ c,
     const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ K,
     const float* __restrict__ dl_dx, const float* __restrict__ dl_du, Bounds bd, float* __restrict__ ws,

@@ -574,8 +574,10 @@ constexpr int packed_cost_floats() { return d * (d + 1) / 2 + d; }
 template <int d>
 constexpr bool packed_diag_ok() { return (2 * d) % 4 == 0; }
 
-// cost_sym[b] flags written by iteration 0
-constexpr unsigned char kCostSym = 1, kCostDiag = 2;
+// cost_sym[b] flags written by iteration 0.  kCostTinv: the packed record is
+// the same, bit for bit, at every t (the reference's callers repeat one
+// diag(q), p over the horizon: il_env.py:159-162, mpc_explicit.py:203-224)
+constexpr unsigned char kCostSym = 1, kCostDiag = 2, kCostTinv = 4;
 
 template <int d>
 DEV void pack_cost(const float (&C)[d][d], const float (&c)[d], float (&buf)[packed_cost_floats<d>()], bool& sym,
@@ -637,6 +639,33 @@ struct CostPacked {
   }
 };
 
+// A diagonal cost that is the same at every t (flags kCostDiag | kCostTinv):
+// its 2d floats are read once per problem, from the packed copy's t = 0
+// record, and every step's load() hands out those registers — the values the
+// per-step read would return, so the arithmetic is unchanged, with no HBM
+// traffic for the cost after iteration 0.
+template <int d>
+struct CostDiagConst {
+  static constexpr bool kDiag = true;
+  float dg[d], cc[d];
+  DEV void init(const float* __restrict__ P, int B, int b) {
+    float Cr[d][d], cr[d];
+    CostPacked<d, true>{P, 1}.load(Cr, cr, 0, B, b);
+#pragma unroll
+    for (int i = 0; i < d; ++i) { dg[i] = Cr[i][i]; cc[i] = cr[i]; }
+  }
+  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t, int, int) const {
+    const float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < d; ++i) {
+#pragma unroll
+      for (int j = 0; j < d; ++j) Cr[i][j] = z;
+      Cr[i][i] = dg[i];
+      cr[i] = cc[i];
+    }
+  }
+};
+
 // The box bounds as a compile-time mode (DILQR_BOUNDS_*): scalar bounds are
 // kernel arguments and per-(t,b) bounds are loaded with the step's other data,
 // so no conditional load exists in the step (a conditional load makes the
@@ -685,6 +714,15 @@ struct FwdIn {
   }
 };
 
+// Prefetch distance of the fused sweep and line search, in steps.  At B =
+// 65536 the one-problem-per-lane kernels run ONE wave per SIMD, so the only
+// latency cover is the loads already in flight.  Two steps ahead measured no
+// faster than one (0.0702 vs 0.0695 ms per iteration, config 2), so 1.
+#ifndef DILQR_PF
+#define DILQR_PF 1
+#endif
+constexpr int kPF = DILQR_PF;
+
 // x, u (current trajectory) and the candidate outputs in layout SOA; the gain
 // records in ws and the packed cost are always float4-column.  ROLLOUT: x is a
 // rollout of the model under u (the MPC slots are), so x_{t+1} = forward(x_t,
@@ -704,24 +742,33 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
   {
     RiccatiState<n, m> rs;
     rs.init();
-    bool sym = true, diag = true;
+    bool sym = true, diag = true, tinv = true;
+    constexpr int PK = packed_cost_floats<d>();
+    float pk_last[PK];                                  // step T-1's packed record (tinv test)
     float xn[n];                                        // x_{t+1} (ROLLOUT)
 #pragma unroll
     for (int i = 0; i < n; ++i) xn[i] = 0.f;
-    SweepIn<n, m, SOA, BM> cur, nxt;
+    // inputs of step t, t-1 (and t-2 at kPF = 2) in flight together
+    SweepIn<n, m, SOA, BM> cur, n1, n2;
     cur.load(cs, x, u, bd, T - 1, B, b);
+    if constexpr (kPF >= 2) n1.load(cs, x, u, bd, T > 1 ? T - 2 : 0, B, b);
     for (int t = T - 1; t >= 0; --t) {
-      nxt.load(cs, x, u, bd, t > 0 ? t - 1 : 0, B, b);                     // prefetch step t-1
+      if constexpr (kPF >= 2) n2.load(cs, x, u, bd, t > 1 ? t - 2 : 0, B, b);   // prefetch step t-2
+      else n1.load(cs, x, u, bd, t > 0 ? t - 1 : 0, B, b);                       // prefetch step t-1
       float tau[d], Ctau[d], cb[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
 #pragma unroll
       for (int a = 0; a < m; ++a) tau[n + a] = cur.u[a];
       if (pack_out) {                                   // first iteration: build the packed copy
-        constexpr int PK = packed_cost_floats<d>();
         float buf[PK];
         pack_cost(cur.C, cur.c, buf, sym, diag);
         SoaRec<PK>::store(pack_out, buf, T, t, B, b);
+#pragma unroll
+        for (int k = 0; k < PK; ++k) {
+          if (t == T - 1) pk_last[k] = buf[k];
+          else tinv &= __float_as_uint(buf[k]) == __float_as_uint(pk_last[k]);
+        }
       }
       float obj = quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau, Ctau);
 #pragma unroll
@@ -758,9 +805,13 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       old_cost += obj;          // summed over t = T-1..0 (the reference's torch sum has its own order)
 #pragma unroll
       for (int i = 0; i < n; ++i) xn[i] = cur.x[i];
-      cur = nxt;
+      cur = n1;
+      if constexpr (kPF >= 2) n1 = n2;
     }
-    if (sym_out) sym_out[b] = sym ? (diag && packed_diag_ok<d>() ? kCostSym | kCostDiag : kCostSym) : 0;
+    if (sym_out)
+      sym_out[b] = sym ? (unsigned char)(kCostSym | (diag && packed_diag_ok<d>() ? kCostDiag : 0) |
+                                         (tinv ? kCostTinv : 0))
+                       : 0;
   }
   // ---------------- forward: the line search (lqr_step_explicit.py:166-263).
   // Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
@@ -780,14 +831,14 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     st_traj<SOA>(xa_out, xA, 0, B, b);
     if (twoB) st_traj<SOA>(xb_out, xB, 0, B, b);
     float cA = 0.f, cB = 0.f;
-    FwdIn<n, m, GREC, SOA, BM> cur, nxt;
-    cur.load(ws, u, cs, x, bd, T, 0, T > 1 ? 1 : 0, B, b);
+    // step s's record holds x_{s+1} of the current trajectory; indices clamp at T-1
+    auto cl = [T](int s) { return s < T ? s : T - 1; };
+    FwdIn<n, m, GREC, SOA, BM> cur, n1, n2;
+    cur.load(ws, u, cs, x, bd, T, 0, cl(1), B, b);
+    if constexpr (kPF >= 2) n1.load(ws, u, cs, x, bd, T, cl(1), cl(2), B, b);
     for (int t = 0; t < T; ++t) {
-      {
-        int t1 = t + 1 < T ? t + 1 : t;                 // prefetch step t+1
-        int t2 = t + 2 < T ? t + 2 : t1;
-        nxt.load(ws, u, cs, x, bd, T, t1, t2, B, b);
-      }
+      if constexpr (kPF >= 2) n2.load(ws, u, cs, x, bd, T, cl(t + 2), cl(t + 3), B, b);   // prefetch step t+2
+      else n1.load(ws, u, cs, x, bd, T, cl(t + 1), cl(t + 2), B, b);                      // prefetch step t+1
       float nuA[m], nuB[m];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
@@ -846,7 +897,8 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
           st_traj<SOA>(xb_out, xB, t + 1, B, b);
         }
       }
-      cur = nxt;
+      cur = n1;
+      if constexpr (kPF >= 2) n1 = n2;
     }
     if (!(cA > old_cost) || p == max_ls - 1) { cost = cA; alpha = aA; win = 0; break; }
     if (!(cB > old_cost) || p + 1 == max_ls - 1) { cost = cB; alpha = aB; win = 1; break; }
@@ -941,7 +993,18 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   // (per-lane flags; a wave normally takes one side of the branch)
   const CostFull<n + m> full{C, c};
   const unsigned char pk = (!first && S.Cpk) ? S.cost_sym[b] : 0;
-  if (pk & kCostDiag) {                  // set by iteration 0 only when packed_diag_ok
+  if ((pk & (kCostDiag | kCostTinv)) == (kCostDiag | kCostTinv)) {
+    if constexpr (packed_diag_ok<n + m>()) {
+      CostDiagConst<n + m> cc;
+      cc.init(S.Cpk, B, b);
+      win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, cc, nullptr, nullptr, S.Xs + cur * TBn,
+                                                S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn,
+                                                S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost,
+                                                alpha);
+    } else {
+      __builtin_unreachable();
+    }
+  } else if (pk & kCostDiag) {           // set by iteration 0 only when packed_diag_ok
     if constexpr (packed_diag_ok<n + m>())
       win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr, nullptr,
                                           S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws,

@@ -187,10 +187,11 @@ def test_fused_iteration_equals_unfused(golden, name):
 # ------------------------------------------------------------------ classic adjoint
 @pytest.mark.parametrize("mname", ["pendulum", "cartpole"])
 def test_packed_cost_paths_bit_identical(mname):
-    """The solve's packed cost copy (diagonal / symmetric / none, chosen per
-    problem by iteration 0) changes only what is read, never the arithmetic: a
-    batch mixing diagonal, dense symmetric and asymmetric C gives bit-identical
-    trajectories and costs with and without the packed copy."""
+    """The solve's packed cost copy (diagonal / symmetric / none, each possibly
+    time-invariant, chosen per problem by iteration 0) changes only what is
+    read, never the arithmetic: a batch mixing time-invariant diagonal,
+    diagonal, time-invariant dense, dense symmetric and asymmetric C gives
+    bit-identical trajectories and costs with and without the packed copy."""
     from dilqr import _native as N
     from dilqr import ops
     dx = dilqr_models()[mname]()
@@ -203,6 +204,9 @@ def test_packed_cost_paths_bit_identical(mname):
     C[:, B // 2:] = C[:, B // 2:] + L @ L.transpose(-1, -2)                       # dense symmetric
     C[:, 3 * B // 4:, 0, 1] += 1e-3                                               # asymmetric
     c = p.repeat(T, B, 1) + 0.01 * torch.randn(T, B, d, generator=g)
+    c[:, :B // 4] = c[0, :B // 4]                                                 # time-invariant diagonal
+    C[:, B // 2:5 * B // 8] = C[0, B // 2:5 * B // 8]                             # time-invariant dense
+    c[:, B // 2:5 * B // 8] = c[0, B // 2:5 * B // 8]
     C, c = C.to(DEV).contiguous(), c.to(DEV).contiguous()
     rng = np.random.RandomState(0)
     if mname == "pendulum":
@@ -225,7 +229,8 @@ def test_packed_cost_paths_bit_identical(mname):
         out.append((x, u, sv.best_cost.clone()))
         if packed:
             flags = cpu(sv.cost_sym)
-            assert (flags[:B // 2] == 3).all() and (flags[B // 2:3 * B // 4] == 1).all()
+            assert (flags[:B // 4] == 7).all() and (flags[B // 4:B // 2] == 3).all()
+            assert (flags[B // 2:5 * B // 8] == 5).all() and (flags[5 * B // 8:3 * B // 4] == 1).all()
             assert (flags[3 * B // 4:] == 0).all()
     for a, b in zip(*out):
         assert torch.equal(a, b)
