@@ -493,14 +493,30 @@ struct RiccatiState {
 // tau . (C tau) so the product is computed once.
 // DIAG: every off-diagonal C entry is +0.0 (the packed diagonal cost), so the
 // row sums reduce to their one nonzero term — the same value the full sum
-// rounds to (adding exact zeros changes nothing but the sign of a zero).
+// rounds to (adding exact zeros changes nothing but the sign of a zero).  The
+// full sum also carries the products +0 * tau_j, which are NaN when some tau_j
+// is inf or NaN; nonfinite_probe() restores that term (NaN for a non-finite
+// tau, a zero otherwise), so a diverged trajectory costs NaN on both paths —
+// and the line search accepts a NaN cost (`cost > old` is false,
+// lqr_step_explicit.py:180, 249) where it would reject +inf.
+template <int D, class S>
+DEV S nonfinite_probe(const S (&tau)[D]) {
+  const S z = S(0.f);
+  S p = z * tau[0];
+#pragma unroll
+  for (int j = 1; j < D; ++j) p = z * tau[j] + p;
+  return p;
+}
+
 template <int D, bool DIAG = false>
 DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D],
                     float (&Ctau)[D]) {
+  float nf = 0.f;
+  if constexpr (DIAG) nf = nonfinite_probe<D>(tau);
 #pragma unroll
   for (int i = 0; i < D; ++i) {
     if constexpr (DIAG) {
-      Ctau[i] = C[i][i] * tau[i];
+      Ctau[i] = C[i][i] * tau[i] + nf;
     } else {
       float s = 0.f;
 #pragma unroll
@@ -519,12 +535,13 @@ DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&t
 
 template <int D, bool DIAG = false>
 DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D]) {
-  float quad = 0.f;
+  float quad = 0.f, nf = 0.f;
+  if constexpr (DIAG) nf = nonfinite_probe<D>(tau);
 #pragma unroll
   for (int j = 0; j < D; ++j) {
     float r = 0.f;
     if constexpr (DIAG) {
-      r = tau[j] * C[j][j];
+      r = tau[j] * C[j][j] + nf;
     } else {
 #pragma unroll
       for (int i = 0; i < D; ++i) r += tau[i] * C[i][j];

@@ -374,20 +374,24 @@ DEV float forward_pass(const DynT& dyn, int T, int B, int b, float alpha, const 
   return cost;
 }
 
+// The current trajectory's cost (lqr_step_explicit.py:171), formed and summed
+// exactly as the fused iteration forms it inside its backward sweep (stage
+// costs as tau . (C tau) + c . tau, summed over t = T-1..0), so the fused and
+// unfused pipelines take the same line-search decisions bit for bit.
 template <int n, int m>
 DEV float traj_cost(int T, int B, int b, const float* __restrict__ C, const float* __restrict__ c,
                     const float* __restrict__ x, const float* __restrict__ u) {
   constexpr int d = n + m;
   float cost = 0.f;
-  for (int t = 0; t < T; ++t) {
+  for (int t = T - 1; t >= 0; --t) {
     size_t tb = (size_t)t * B + b;
-    float Ct[d][d], ct[d], tau[d], xt[n], ut[m];
+    float Ct[d][d], ct[d], tau[d], xt[n], ut[m], Ctau[d];
     ld2(Ct, C + tb * d * d); ld(ct, c + tb * d); ld(xt, x + tb * n); ld(ut, u + tb * m);
 #pragma unroll
     for (int i = 0; i < n; ++i) tau[i] = xt[i];
 #pragma unroll
     for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
-    cost += quad_cost(Ct, ct, tau);
+    cost += quad_cost(Ct, ct, tau, Ctau);
   }
   return cost;
 }
@@ -597,13 +601,17 @@ DEV void pack_cost(const float (&C)[d][d], const float (&c)[d], float (&buf)[pac
     }
 }
 
-template <int d, bool DIAG = false>
+// TINV: a time-invariant cost (flag kCostTinv) whose copy holds ONE record,
+// t = T-1 (iteration 0 writes the others only once the cost changes over t);
+// every step reads that record.
+template <int d, bool DIAG = false, bool TINV = false>
 struct CostPacked {
   static constexpr bool kDiag = DIAG;
   const float* __restrict__ P;
   int T;
-  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t, int B, int b) const {
+  DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t_, int B, int b) const {
     constexpr int PK = packed_cost_floats<d>();
+    const size_t t = TINV ? (size_t)(T - 1) : t_;
     if constexpr (DIAG) {
       static_assert(packed_diag_ok<d>(), "diagonal read needs whole float4 planes");
       constexpr int Q4 = SoaRec<PK>::Q4;
@@ -640,19 +648,25 @@ struct CostPacked {
 };
 
 // A diagonal cost that is the same at every t (flags kCostDiag | kCostTinv):
-// its 2d floats are read once per problem, from the packed copy's t = 0
-// record, and every step's load() hands out those registers — the values the
-// per-step read would return, so the arithmetic is unchanged, with no HBM
-// traffic for the cost after iteration 0.
+// its 2d floats are read once per problem (the copy's one record, t = T-1) or
+// handed over from registers by the iteration that built the copy, and every
+// step's load() hands out those registers — the values the per-step read would
+// return, so the arithmetic is unchanged, with no HBM traffic for the cost.
 template <int d>
 struct CostDiagConst {
   static constexpr bool kDiag = true;
   float dg[d], cc[d];
-  DEV void init(const float* __restrict__ P, int B, int b) {
+  DEV void init(const float* __restrict__ P, int T, int B, int b) {
     float Cr[d][d], cr[d];
-    CostPacked<d, true>{P, 1}.load(Cr, cr, 0, B, b);
+    CostPacked<d, true>{P, T}.load(Cr, cr, T - 1, B, b);
 #pragma unroll
     for (int i = 0; i < d; ++i) { dg[i] = Cr[i][i]; cc[i] = cr[i]; }
+  }
+  // from a packed record held in registers (diag, then c, ...)
+  template <int PK>
+  DEV void set(const float (&pk)[PK]) {
+#pragma unroll
+    for (int i = 0; i < d; ++i) { dg[i] = pk[i]; cc[i] = pk[d + i]; }
   }
   DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t, int, int) const {
     const float z = 0.f;
@@ -723,102 +737,20 @@ struct FwdIn {
 #endif
 constexpr int kPF = DILQR_PF;
 
-// x, u (current trajectory) and the candidate outputs in layout SOA; the gain
-// records in ws and the packed cost are always float4-column.  ROLLOUT: x is a
-// rollout of the model under u (the MPC slots are), so x_{t+1} = forward(x_t,
-// u_t) bit for bit and models with kJacFromNext take part of the Jacobian from it.
-template <class Model, int BM, bool SOA, bool ROLLOUT, class CostT>
-DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
-                     float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
-                     const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
-                     float* __restrict__ ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
-                     float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
-                     float& cost_out, float& alpha_out) {
+// ---------------- forward: the line search (lqr_step_explicit.py:166-263).
+// Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
+// it is the last pass.  Passes 2r and 2r+1 roll out TOGETHER (candidates A
+// and B), sharing every load of the step; the first accepted candidate wins,
+// which is exactly the sequential search.  A wave otherwise pays a whole
+// second latency-bound pass whenever any of its 64 problems backtracks.
+template <class Model, int BM, bool SOA, class CostT>
+DEV int line_search(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
+                    const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd, float decay,
+                    int max_ls, const float* __restrict__ ws, float* __restrict__ xa_out,
+                    float* __restrict__ ua_out, float* __restrict__ xb_out, float* __restrict__ ub_out,
+                    float* __restrict__ du_sq, float old_cost, float& cost_out, float& alpha_out) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
-  constexpr int MODE = BM == DILQR_BOUNDS_NONE ? GAIN_UNC : GAIN_BOX;
   constexpr int GREC = m * n + m;                    // gain record: K, k (component-major)
-  float old_cost = 0.f;                               // the current trajectory's cost, from the sweep
-  // ---------------- backward: linearise + Riccati + stage costs of the current trajectory
-  {
-    RiccatiState<n, m> rs;
-    rs.init();
-    bool sym = true, diag = true, tinv = true;
-    constexpr int PK = packed_cost_floats<d>();
-    float pk_last[PK];                                  // step T-1's packed record (tinv test)
-    float xn[n];                                        // x_{t+1} (ROLLOUT)
-#pragma unroll
-    for (int i = 0; i < n; ++i) xn[i] = 0.f;
-    // inputs of step t, t-1 (and t-2 at kPF = 2) in flight together
-    SweepIn<n, m, SOA, BM> cur, n1, n2;
-    cur.load(cs, x, u, bd, T - 1, B, b);
-    if constexpr (kPF >= 2) n1.load(cs, x, u, bd, T > 1 ? T - 2 : 0, B, b);
-    for (int t = T - 1; t >= 0; --t) {
-      if constexpr (kPF >= 2) n2.load(cs, x, u, bd, t > 1 ? t - 2 : 0, B, b);   // prefetch step t-2
-      else n1.load(cs, x, u, bd, t > 0 ? t - 1 : 0, B, b);                       // prefetch step t-1
-      float tau[d], Ctau[d], cb[d];
-#pragma unroll
-      for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
-#pragma unroll
-      for (int a = 0; a < m; ++a) tau[n + a] = cur.u[a];
-      if (pack_out) {                                   // first iteration: build the packed copy
-        float buf[PK];
-        pack_cost(cur.C, cur.c, buf, sym, diag);
-        SoaRec<PK>::store(pack_out, buf, T, t, B, b);
-#pragma unroll
-        for (int k = 0; k < PK; ++k) {
-          if (t == T - 1) pk_last[k] = buf[k];
-          else tinv &= __float_as_uint(buf[k]) == __float_as_uint(pk_last[k]);
-        }
-      }
-      float obj = quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau, Ctau);
-#pragma unroll
-      for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + cur.c[i];
-      float Ft[n][d];
-      if (t < T - 1) {
-        if constexpr (ROLLOUT && Model::kJacFromNext) md.jacobian_next(cur.x, cur.u, xn, Ft);
-        else md.jacobian(cur.x, cur.u, Ft);
-      } else {
-#pragma unroll
-        for (int i = 0; i < n; ++i)
-#pragma unroll
-          for (int j = 0; j < d; ++j) Ft[i][j] = 0.f;
-      }
-      float zIt[m], lb[m], ub[m];
-#pragma unroll
-      for (int a = 0; a < m; ++a) {
-        zIt[a] = 0.f; lb[a] = 0.f; ub[a] = 0.f;
-        if constexpr (MODE == GAIN_BOX) {
-          lb[a] = cur.bnd.l(bd, a) - cur.u[a];
-          ub[a] = cur.bnd.h(bd, a) - cur.u[a];
-        }
-      }
-      float Kt[m][n], kt[m];
-      rs.template step<MODE, typename Model::FSparsity, CostT::kDiag>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
-      float g[GREC];
-#pragma unroll
-      for (int a = 0; a < m; ++a) {
-#pragma unroll
-        for (int j = 0; j < n; ++j) g[a * n + j] = Kt[a][j];
-        g[m * n + a] = kt[a];
-      }
-      SoaRec<GREC>::store(ws, g, T, t, B, b);
-      old_cost += obj;          // summed over t = T-1..0 (the reference's torch sum has its own order)
-#pragma unroll
-      for (int i = 0; i < n; ++i) xn[i] = cur.x[i];
-      cur = n1;
-      if constexpr (kPF >= 2) n1 = n2;
-    }
-    if (sym_out)
-      sym_out[b] = sym ? (unsigned char)(kCostSym | (diag && packed_diag_ok<d>() ? kCostDiag : 0) |
-                                         (tinv ? kCostTinv : 0))
-                       : 0;
-  }
-  // ---------------- forward: the line search (lqr_step_explicit.py:166-263).
-  // Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
-  // it is the last pass.  Passes 2r and 2r+1 roll out TOGETHER (candidates A
-  // and B), sharing every load of the step; the first accepted candidate wins,
-  // which is exactly the sequential search.  A wave otherwise pays a whole
-  // second latency-bound pass whenever any of its 64 problems backtracks.
   float alpha = 1.f, cost = 0.f;
   int win = 0;
   for (int p = 0; p < max_ls; p += 2) {
@@ -909,6 +841,120 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
   return win;
 }
 
+// x, u (current trajectory) and the candidate outputs in layout SOA; the gain
+// records in ws and the packed cost are always float4-column.  ROLLOUT: x is a
+// rollout of the model under u (the MPC slots are), so x_{t+1} = forward(x_t,
+// u_t) bit for bit and models with kJacFromNext take part of the Jacobian from it.
+// pack_out (iteration 0 of a solve): build the packed cost copy while the sweep
+// reads C.  A time-invariant cost is stored as its t = T-1 record only (the
+// records a later change of the cost proves necessary are written then, from
+// the registers holding that record), and a time-invariant diagonal cost is
+// handed to this iteration's line search in registers, so C is read once.
+template <class Model, int BM, bool SOA, bool ROLLOUT, class CostT>
+DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
+                     float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
+                     const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
+                     float* __restrict__ ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
+                     float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
+                     float& cost_out, float& alpha_out) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  constexpr int MODE = BM == DILQR_BOUNDS_NONE ? GAIN_UNC : GAIN_BOX;
+  constexpr int GREC = m * n + m;                    // gain record: K, k (component-major)
+  constexpr int PK = packed_cost_floats<d>();
+  float old_cost = 0.f;                               // the current trajectory's cost, from the sweep
+  bool sym = true, diag = true, tinv = true;
+  float pk_last[PK];                                  // step T-1's packed record (tinv test)
+  // ---------------- backward: linearise + Riccati + stage costs of the current trajectory
+  {
+    RiccatiState<n, m> rs;
+    rs.init();
+    float xn[n];                                        // x_{t+1} (ROLLOUT)
+#pragma unroll
+    for (int i = 0; i < n; ++i) xn[i] = 0.f;
+    // inputs of step t, t-1 (and t-2 at kPF = 2) in flight together
+    SweepIn<n, m, SOA, BM> cur, n1, n2;
+    cur.load(cs, x, u, bd, T - 1, B, b);
+    if constexpr (kPF >= 2) n1.load(cs, x, u, bd, T > 1 ? T - 2 : 0, B, b);
+    for (int t = T - 1; t >= 0; --t) {
+      if constexpr (kPF >= 2) n2.load(cs, x, u, bd, t > 1 ? t - 2 : 0, B, b);   // prefetch step t-2
+      else n1.load(cs, x, u, bd, t > 0 ? t - 1 : 0, B, b);                       // prefetch step t-1
+      float tau[d], Ctau[d], cb[d];
+#pragma unroll
+      for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) tau[n + a] = cur.u[a];
+      if (pack_out) {                                   // first iteration: build the packed copy
+        float buf[PK];
+        pack_cost(cur.C, cur.c, buf, sym, diag);
+        if (t == T - 1) {
+          SoaRec<PK>::store(pack_out, buf, T, t, B, b);
+#pragma unroll
+          for (int k = 0; k < PK; ++k) pk_last[k] = buf[k];
+        } else {
+          bool same = true;
+#pragma unroll
+          for (int k = 0; k < PK; ++k) same &= __float_as_uint(buf[k]) == __float_as_uint(pk_last[k]);
+          if (tinv && !same)                            // records t+1 .. T-2 were skipped: all equal step T-1's
+            for (int s = t + 1; s < T - 1; ++s) SoaRec<PK>::store(pack_out, pk_last, T, s, B, b);
+          tinv &= same;
+          if (!tinv) SoaRec<PK>::store(pack_out, buf, T, t, B, b);
+        }
+      }
+      float obj = quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau, Ctau);
+#pragma unroll
+      for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + cur.c[i];
+      float Ft[n][d];
+      if (t < T - 1) {
+        if constexpr (ROLLOUT && Model::kJacFromNext) md.jacobian_next(cur.x, cur.u, xn, Ft);
+        else md.jacobian(cur.x, cur.u, Ft);
+      } else {
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int j = 0; j < d; ++j) Ft[i][j] = 0.f;
+      }
+      float zIt[m], lb[m], ub[m];
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        zIt[a] = 0.f; lb[a] = 0.f; ub[a] = 0.f;
+        if constexpr (MODE == GAIN_BOX) {
+          lb[a] = cur.bnd.l(bd, a) - cur.u[a];
+          ub[a] = cur.bnd.h(bd, a) - cur.u[a];
+        }
+      }
+      float Kt[m][n], kt[m];
+      rs.template step<MODE, typename Model::FSparsity, CostT::kDiag>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
+      float g[GREC];
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+#pragma unroll
+        for (int j = 0; j < n; ++j) g[a * n + j] = Kt[a][j];
+        g[m * n + a] = kt[a];
+      }
+      SoaRec<GREC>::store(ws, g, T, t, B, b);
+      old_cost += obj;          // summed over t = T-1..0 (the reference's torch sum has its own order)
+#pragma unroll
+      for (int i = 0; i < n; ++i) xn[i] = cur.x[i];
+      cur = n1;
+      if constexpr (kPF >= 2) n1 = n2;
+    }
+    if (sym_out)
+      sym_out[b] = sym ? (unsigned char)(kCostSym | (diag && packed_diag_ok<d>() ? kCostDiag : 0) |
+                                         (tinv ? kCostTinv : 0))
+                       : 0;
+  }
+  if constexpr (!CostT::kDiag && packed_diag_ok<d>()) {
+    if (pack_out && sym && diag && tinv) {              // iteration 0 of a diag(q), p over t cost
+      CostDiagConst<d> cc;
+      cc.set(pk_last);
+      return line_search<Model, BM, SOA>(T, B, b, md, x_init, cc, x, u, bd, decay, max_ls, ws, xa_out, ua_out,
+                                         xb_out, ub_out, du_sq, old_cost, cost_out, alpha_out);
+    }
+  }
+  return line_search<Model, BM, SOA>(T, B, b, md, x_init, cs, x, u, bd, decay, max_ls, ws, xa_out, ua_out, xb_out,
+                                     ub_out, du_sq, old_cost, cost_out, alpha_out);
+}
+
 template <class Model, int BM>
 __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const float* __restrict__ theta,
                                                          const float* __restrict__ x_init, const float* __restrict__ C,
@@ -996,7 +1042,7 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   if ((pk & (kCostDiag | kCostTinv)) == (kCostDiag | kCostTinv)) {
     if constexpr (packed_diag_ok<n + m>()) {
       CostDiagConst<n + m> cc;
-      cc.init(S.Cpk, B, b);
+      cc.init(S.Cpk, T, B, b);
       win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, cc, nullptr, nullptr, S.Xs + cur * TBn,
                                                 S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn,
                                                 S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost,
@@ -1012,7 +1058,12 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
                                           S.du_sq, cost, alpha);
     else
       __builtin_unreachable();
-  } else if (pk & kCostSym)
+  } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
+    win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T}, nullptr,
+                                    nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws,
+                                    S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq,
+                                    cost, alpha);
+  else if (pk & kCostSym)
     win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
                                     S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn,
                                     S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost, alpha);

@@ -231,7 +231,13 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
    Later iterations of flagged problems read the copy: 27 instead of 42 floats
    per step at d=6, or 12 for a diagonal cost (diag(q), the reference's own
    callers, il_env.py:159-162); identical arithmetic.  The cost passed to the
-   iterations of one solve must not change. */
+   iterations of one solve must not change.
+   Invariant: every trajectory held in a slot is a rollout of the model, i.e.
+   x_{t+1} == forward(x_t, u_t) bit for bit with u_t as stored (already
+   clamped to the box) — begin and the line search write only such
+   trajectories.  The fused sweep relies on it: models whose Jacobian needs the
+   integrated angle's cos/sin (cartpole) take them from x_{t+1} instead of
+   recomputing atan2, cos and sin.  Do not write into Xs/Us from outside. */
 typedef struct dilqr_mpc_state {
   float* Xs; float* Us; unsigned char* slot; float* best_cost; float* best_du;
   int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;
