@@ -25,6 +25,32 @@ namespace dilqr {
 // ops (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32), two FMAs per lane per issue
 typedef float f2 __attribute__((ext_vector_type(2)));
 
+// Scalar-generic elementary functions: the model code is written once for a
+// float and for an f2 holding the same quantity of two independent
+// trajectories (the line search's two candidates).  Each f2 component gets
+// exactly the float operation (IEEE +,-,*,/ per component; the libm calls per
+// component), so a packed evaluation rounds like two scalar ones.
+DEV float vatan2(float y, float x) { return atan2f(y, x); }
+DEV f2 vatan2(f2 y, f2 x) { return f2{atan2f(y.x, x.x), atan2f(y.y, x.y)}; }
+DEV float vcos(float x) { return cosf(x); }
+DEV f2 vcos(f2 x) { return f2{cosf(x.x), cosf(x.y)}; }
+DEV float vsin(float x) { return sinf(x); }
+DEV f2 vsin(f2 x) { return f2{sinf(x.x), sinf(x.y)}; }
+// sin and cos of one angle with one argument reduction (ocml's sincos shares
+// sin's and cos's reduction and polynomials: bit-identical to sinf/cosf —
+// checked over 6.1e8 inputs spanning every exponent by
+// tools/microbench/sincos_bits.hip on MI355X)
+DEV void vsincos(float x, float& s, float& c) { sincosf(x, &s, &c); }
+DEV void vsincos(f2 x, f2& s, f2& c) {
+  float s0, c0, s1, c1;
+  sincosf(x.x, &s0, &c0);
+  sincosf(x.y, &s1, &c1);
+  s = f2{s0, s1};
+  c = f2{c0, c1};
+}
+DEV float vclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+DEV f2 vclamp(f2 x, float lo, float hi) { return f2{fminf(fmaxf(x.x, lo), hi), fminf(fmaxf(x.y, lo), hi)}; }
+
 // ------------------------------------------------------------------ loads/stores
 // Vectorised load/store of one lane's contiguous record of K floats.  Record
 // offsets are multiples of K floats and the base is 16-byte aligned (checked on
@@ -306,6 +332,16 @@ struct DenseF {
   static constexpr bool nz(int, int) { return true; }
 };
 
+template <int D>
+DEV bool bitwise_symmetric(const float (&C)[D][D]) {
+  bool sym = true;
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = i + 1; j < D; ++j) sym &= __float_as_uint(C[i][j]) == __float_as_uint(C[j][i]);
+  return sym;
+}
+
 template <int N, int M>
 struct RiccatiState {
   static constexpr int D = N + M;
@@ -330,33 +366,70 @@ struct RiccatiState {
 
   // mode GAIN_ZERO_I uses zI[M] (1 = active); GAIN_BOX uses lb/ub [M] (already
   // lower-u_t / upper-u_t, lqr_step_explicit.py:132-133).
-  template <int MODE, class FS = DenseF, bool DIAG = false>
+  // SYM: C_t and every later C are bitwise symmetric (so V_{t+1} is, as this
+  // mode keeps it): F^T V F is formed as F^T (V F) on and above the diagonal
+  // and mirrored, and V_t likewise — the products of the upper triangle only
+  // (cartpole: 118 instead of 187 for Q, 15 instead of 25 entries of V).  The
+  // mirrored entries are the exact-arithmetic values; in fp32 they differ from
+  // the full products by rounding, as any two summation orders do.  Every
+  // caller that must agree bit for bit (the fused and the unfused sweep) picks
+  // SYM by the same rule: all C_t' (t' >= t) of the problem bitwise symmetric.
+  template <int MODE, class FS = DenseF, bool DIAG = false, bool SYM = false>
   DEV void step(const float (&C)[D][D], const float (&cb)[D], const float (&F)[N][D],
                 const float (&zI)[M], const float (&lb)[M], const float (&ub)[M],
                 float (&K)[M][N], float (&k)[M]) {
-    // Q = C + (F^T V) F,  q = cb + F^T v   (lqr_step_explicit.py:68-72)
-    float P[D][N];
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int kk = 0; kk < N; ++kk) {
-        float s = 0.f;
-#pragma unroll
-        for (int l = 0; l < N; ++l)
-          if (FS::nz(l, i)) s += F[l][i] * V[l][kk];
-        P[i][kk] = s;
-      }
     float Q[D][D], q[D];
+    if constexpr (SYM) {
+      // W = V F (N x D), S = F^T W on and above the diagonal
+      float W[N][D];
+#pragma unroll
+      for (int l = 0; l < N; ++l)
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int kk = 0; kk < N; ++kk)
+            if (FS::nz(kk, j)) s += V[l][kk] * F[kk][j];
+          W[l][j] = s;
+        }
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int j = i; j < D; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int l = 0; l < N; ++l)
+            if (FS::nz(l, i)) s += F[l][i] * W[l][j];
+          Q[i][j] = (DIAG && i != j) ? s : C[i][j] + s;     // DIAG: C[i][j] is +0.0
+          if (j != i) Q[j][i] = (DIAG) ? s : C[j][i] + s;
+        }
+    } else {
+      // Q = C + (F^T V) F   (lqr_step_explicit.py:68-72)
+      float P[D][N];
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int kk = 0; kk < N; ++kk) {
+          float s = 0.f;
+#pragma unroll
+          for (int l = 0; l < N; ++l)
+            if (FS::nz(l, i)) s += F[l][i] * V[l][kk];
+          P[i][kk] = s;
+        }
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int kk = 0; kk < N; ++kk)
+            if (FS::nz(kk, j)) s += P[i][kk] * F[kk][j];
+          Q[i][j] = (DIAG && i != j) ? s : C[i][j] + s;     // DIAG: C[i][j] is +0.0
+        }
+    }
+    // q = cb + F^T v
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-#pragma unroll
-      for (int j = 0; j < D; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int kk = 0; kk < N; ++kk)
-          if (FS::nz(kk, j)) s += P[i][kk] * F[kk][j];
-        Q[i][j] = (DIAG && i != j) ? s : C[i][j] + s;     // DIAG: C[i][j] is +0.0
-      }
       float s = 0.f;
 #pragma unroll
       for (int l = 0; l < N; ++l)
@@ -466,7 +539,7 @@ struct RiccatiState {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
+      for (int j = SYM ? i : 0; j < N; ++j) {
         float s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
         for (int a = 0; a < M; ++a) {
@@ -475,6 +548,7 @@ struct RiccatiState {
           s3 += KtQuu[i][a] * K[a][j];
         }
         V[i][j] = ((Q[i][j] + s1) + s2) + s3;
+        if (SYM && j != i) V[j][i] = V[i][j];
       }
       float s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
@@ -533,13 +607,15 @@ DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&t
   return 0.5f * quad + lin;
 }
 
-template <int D, bool DIAG = false>
-DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D]) {
-  float quad = 0.f, nf = 0.f;
+// The stage cost alone, as tau . (tau^T C) (columns); S = float, or f2 for two
+// trajectories at once (each component rounds like the float evaluation).
+template <int D, bool DIAG = false, class S = float>
+DEV S quad_cost(const float (&C)[D][D], const float (&c)[D], const S (&tau)[D]) {
+  S quad = S(0.f), nf = S(0.f);
   if constexpr (DIAG) nf = nonfinite_probe<D>(tau);
 #pragma unroll
   for (int j = 0; j < D; ++j) {
-    float r = 0.f;
+    S r = S(0.f);
     if constexpr (DIAG) {
       r = tau[j] * C[j][j] + nf;
     } else {
@@ -548,7 +624,7 @@ DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&t
     }
     quad += r * tau[j];
   }
-  float lin = 0.f;
+  S lin = S(0.f);
 #pragma unroll
   for (int i = 0; i < D; ++i) lin += tau[i] * c[i];
   return 0.5f * quad + lin;

@@ -194,6 +194,7 @@ __global__ void __launch_bounds__(kBlock) k_lqr_backward(int T, int B, const flo
   if (b >= B) return;
   RiccatiState<n, m> rs;
   rs.init();
+  bool symsofar = true;
   // per-step inputs, software-pipelined one step ahead (see ilqr_problem)
   struct In {
     float C[d][d], c[d], F[n][d], x[n], u[m];
@@ -250,7 +251,9 @@ __global__ void __launch_bounds__(kBlock) k_lqr_backward(int T, int B, const flo
       }
     }
     float Kt[m][n], kt[m];
-    rs.template step<MODE>(cur.C, cb, cur.F, zIt, lb, ub, Kt, kt);
+    symsofar &= bitwise_symmetric(cur.C);              // the fused sweep's rule (RiccatiState SYM)
+    if (symsofar) rs.template step<MODE, DenseF, false, true>(cur.C, cb, cur.F, zIt, lb, ub, Kt, kt);
+    else rs.template step<MODE>(cur.C, cb, cur.F, zIt, lb, ub, Kt, kt);
     st2(K + tb * m * n, Kt);
     st(k + tb * m, kt);
     cur = nxt;
@@ -564,6 +567,7 @@ DEV void st_traj(float* __restrict__ p, const float (&r)[K], size_t t, int B, in
 template <int d>
 struct CostFull {
   static constexpr bool kDiag = false;
+  static constexpr bool kSym = false;      // symmetry is tested per step at run time
   const float* __restrict__ C;
   const float* __restrict__ c;
   DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t, int B, int b) const {
@@ -607,6 +611,7 @@ DEV void pack_cost(const float (&C)[d][d], const float (&c)[d], float (&buf)[pac
 template <int d, bool DIAG = false, bool TINV = false>
 struct CostPacked {
   static constexpr bool kDiag = DIAG;
+  static constexpr bool kSym = true;
   const float* __restrict__ P;
   int T;
   DEV void load(float (&Cr)[d][d], float (&cr)[d], size_t t_, int B, int b) const {
@@ -655,6 +660,7 @@ struct CostPacked {
 template <int d>
 struct CostDiagConst {
   static constexpr bool kDiag = true;
+  static constexpr bool kSym = true;
   float dg[d], cc[d];
   DEV void init(const float* __restrict__ P, int T, int B, int b) {
     float Cr[d][d], cr[d];
@@ -753,16 +759,26 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
   constexpr int GREC = m * n + m;                    // gain record: K, k (component-major)
   float alpha = 1.f, cost = 0.f;
   int win = 0;
+  // Candidates A and B travel as the two components of f2 values: every
+  // arithmetic step of the pair is one packed instruction (v_pk_fma_f32 /
+  // v_pk_mul_f32 / v_pk_add_f32), and each component rounds exactly like the
+  // scalar rollout of that candidate.  (Measured alternatives that were
+  // slower on MI355X: unrolling the step loop twice over two prefetch buffers
+  // and making every store unconditional, +3 us per iteration.)
   for (int p = 0; p < max_ls; p += 2) {
     const bool twoB = p + 1 < max_ls;                       // uniform
     const float aA = alpha, aB = alpha * decay;
-    float xA[n], dA[n], xB[n], dB[n];
-    ld(xA, x_init + (size_t)b * n);
+    const f2 al = {aA, aB};
+    f2 xp[n], dp[n];
+    {
+      float x0[n];
+      ld(x0, x_init + (size_t)b * n);
 #pragma unroll
-    for (int i = 0; i < n; ++i) { dA[i] = 0.f; xB[i] = xA[i]; dB[i] = 0.f; }
-    st_traj<SOA>(xa_out, xA, 0, B, b);
-    if (twoB) st_traj<SOA>(xb_out, xB, 0, B, b);
-    float cA = 0.f, cB = 0.f;
+      for (int i = 0; i < n; ++i) { xp[i] = f2{x0[i], x0[i]}; dp[i] = f2{0.f, 0.f}; }
+      st_traj<SOA>(xa_out, x0, 0, B, b);
+      if (twoB) st_traj<SOA>(xb_out, x0, 0, B, b);
+    }
+    f2 cp = {0.f, 0.f};
     // step s's record holds x_{s+1} of the current trajectory; indices clamp at T-1
     auto cl = [T](int s) { return s < T ? s : T - 1; };
     FwdIn<n, m, GREC, SOA, BM> cur, n1, n2;
@@ -771,67 +787,56 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
     for (int t = 0; t < T; ++t) {
       if constexpr (kPF >= 2) n2.load(ws, u, cs, x, bd, T, cl(t + 2), cl(t + 3), B, b);   // prefetch step t+2
       else n1.load(ws, u, cs, x, bd, T, cl(t + 1), cl(t + 2), B, b);                      // prefetch step t+1
-      float nuA[m], nuB[m];
+      f2 nu[m];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
-        float sA = 0.f, sB = 0.f;
+        f2 sp = {0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < n; ++j) {
-          sA += cur.g[a * n + j] * dA[j];
-          sB += cur.g[a * n + j] * dB[j];
-        }
-        nuA[a] = (sA + cur.u[a]) + aA * cur.g[m * n + a];
-        nuB[a] = (sB + cur.u[a]) + aB * cur.g[m * n + a];
+        for (int j = 0; j < n; ++j) sp += cur.g[a * n + j] * dp[j];
+        nu[a] = (sp + cur.u[a]) + al * cur.g[m * n + a];
         if constexpr (BM != DILQR_BOUNDS_NONE) {
           const float lo = cur.bnd.l(bd, a), hi = cur.bnd.h(bd, a);
-          nuA[a] = eclamp(nuA[a], lo, hi);
-          nuB[a] = eclamp(nuB[a], lo, hi);
+          nu[a] = f2{eclamp(nu[a].x, lo, hi), eclamp(nu[a].y, lo, hi)};
         }
       }
-      st_traj<SOA>(ua_out, nuA, t, B, b);
-      if (twoB) st_traj<SOA>(ub_out, nuB, t, B, b);
+      {
+        float ua[m], ub[m];
+#pragma unroll
+        for (int a = 0; a < m; ++a) { ua[a] = nu[a].x; ub[a] = nu[a].y; }
+        st_traj<SOA>(ua_out, ua, t, B, b);
+        if (twoB) st_traj<SOA>(ub_out, ub, t, B, b);
+      }
       if (p == 0) {
 #pragma unroll
         for (int a = 0; a < m; ++a) {
-          float e = cur.u[a] - nuA[a];
+          float e = cur.u[a] - nu[a].x;
           du_sq[((size_t)t * m + a) * B + b] = e * e;
         }
       }
-      float tau[d];
+      f2 tau[d];
 #pragma unroll
-      for (int i = 0; i < n; ++i) tau[i] = xA[i];
+      for (int i = 0; i < n; ++i) tau[i] = xp[i];
 #pragma unroll
-      for (int a = 0; a < m; ++a) tau[n + a] = nuA[a];
-      cA += quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau);
-      if (twoB) {
-#pragma unroll
-        for (int i = 0; i < n; ++i) tau[i] = xB[i];
-#pragma unroll
-        for (int a = 0; a < m; ++a) tau[n + a] = nuB[a];
-        cB += quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau);
-      }
+      for (int a = 0; a < m; ++a) tau[n + a] = nu[a];
+      cp += quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau);
       if (t < T - 1) {
-        float xnext[n];
-        md.forward(xA, nuA, xnext);
+        f2 xnext[n];
+        md.forward(xp, nu, xnext);
+        float xa[n], xb[n];
 #pragma unroll
         for (int i = 0; i < n; ++i) {
-          dA[i] = xnext[i] - cur.xnext[i];
-          xA[i] = xnext[i];
+          dp[i] = xnext[i] - cur.xnext[i];
+          xp[i] = xnext[i];
+          xa[i] = xnext[i].x;
+          xb[i] = xnext[i].y;
         }
-        st_traj<SOA>(xa_out, xA, t + 1, B, b);
-        if (twoB) {
-          md.forward(xB, nuB, xnext);
-#pragma unroll
-          for (int i = 0; i < n; ++i) {
-            dB[i] = xnext[i] - cur.xnext[i];
-            xB[i] = xnext[i];
-          }
-          st_traj<SOA>(xb_out, xB, t + 1, B, b);
-        }
+        st_traj<SOA>(xa_out, xa, t + 1, B, b);
+        if (twoB) st_traj<SOA>(xb_out, xb, t + 1, B, b);
       }
       cur = n1;
       if constexpr (kPF >= 2) n1 = n2;
     }
+    const float cA = cp.x, cB = cp.y;
     if (!(cA > old_cost) || p == max_ls - 1) { cost = cA; alpha = aA; win = 0; break; }
     if (!(cB > old_cost) || p + 1 == max_ls - 1) { cost = cB; alpha = aB; win = 1; break; }
     alpha = aB * decay;                                     // lqr_step_explicit.py:249
@@ -863,6 +868,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
   constexpr int PK = packed_cost_floats<d>();
   float old_cost = 0.f;                               // the current trajectory's cost, from the sweep
   bool sym = true, diag = true, tinv = true;
+  bool symsofar = true;                               // C_t' bitwise symmetric for all t' >= t (RiccatiState SYM)
   float pk_last[PK];                                  // step T-1's packed record (tinv test)
   // ---------------- backward: linearise + Riccati + stage costs of the current trajectory
   {
@@ -923,7 +929,14 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
         }
       }
       float Kt[m][n], kt[m];
-      rs.template step<MODE, typename Model::FSparsity, CostT::kDiag>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
+      using FS = typename Model::FSparsity;
+      if constexpr (CostT::kSym) {
+        rs.template step<MODE, FS, CostT::kDiag, true>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
+      } else {
+        symsofar &= bitwise_symmetric(cur.C);
+        if (symsofar) rs.template step<MODE, FS, CostT::kDiag, true>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
+        else rs.template step<MODE, FS, CostT::kDiag, false>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
+      }
       float g[GREC];
 #pragma unroll
       for (int a = 0; a < m; ++a) {

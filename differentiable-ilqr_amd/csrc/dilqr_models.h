@@ -27,18 +27,18 @@ struct Pendulum {
     static constexpr bool nz(int i, int j) { return !(i == 2 && j == 0); }
   };
 
-  // pendulum.py:60-95
-  DEV void forward(const float (&x)[N], const float (&u)[M], float (&o)[N]) const {
+  // pendulum.py:60-95; S = float, or f2 for two trajectories at once
+  template <class S>
+  DEV void forward(const S (&x)[N], const S (&u)[M], S (&o)[N]) const {
 #pragma clang fp contract(off)
-    float uu = fminf(fmaxf(u[0], -2.0f), 2.0f);
-    float c = x[0], s = x[1], dth = x[2];
-    float th = atan2f(s, c);
-    float a = (-3.0f * g) / (2.0f * l) * (-s);
-    float b = (3.0f * uu) / (m * (l * l));
-    float newdth = dth + DT * (a + b);
-    float newth = th + newdth * DT;
-    o[0] = cosf(newth);
-    o[1] = sinf(newth);
+    S uu = vclamp(u[0], -2.0f, 2.0f);
+    S c = x[0], s = x[1], dth = x[2];
+    S th = vatan2(s, c);
+    S a = (-3.0f * g) / (2.0f * l) * (-s);
+    S b = (3.0f * uu) / (m * (l * l));
+    S newdth = dth + DT * (a + b);
+    S newth = th + newdth * DT;
+    vsincos(newth, o[1], o[0]);
     o[2] = newdth;
   }
 
@@ -49,7 +49,8 @@ struct Pendulum {
     float kg = 3.0f * g / (2.0f * l);
     float ku = 3.0f / (l * l * m);
     float newth = DT * (DT * (kg * s + ku * uu) + dth) + atan2f(s, c);
-    float sn = sinf(newth), cs = cosf(newth);
+    float sn, cs;
+    vsincos(newth, sn, cs);
     float dc = -s / r2;                 // d newth / d cos
     float ds = c / r2 + DT * DT * kg;   // d newth / d sin
     float dw = DT;                      // d newth / d dth
@@ -77,22 +78,22 @@ struct Cartpole {
     }
   };
 
-  // cartpole.py:64-97
-  DEV void forward(const float (&s_)[N], const float (&u)[M], float (&o)[N]) const {
+  // cartpole.py:64-97; S = float, or f2 for two trajectories at once
+  template <class S>
+  DEV void forward(const S (&s_)[N], const S (&u)[M], S (&o)[N]) const {
 #pragma clang fp contract(off)
     float total_mass = mp + mc;
     float pml = mp * l;
-    float uu = fminf(fmaxf(u[0], -100.0f), 100.0f);
-    float x = s_[0], dx = s_[1], c = s_[2], s = s_[3], dth = s_[4];
-    float th = atan2f(s, c);
-    float cart_in = (uu + (pml * (dth * dth)) * s) / total_mass;
-    float th_acc = (g * s - c * cart_in) / (l * (4.0f / 3.0f - (mp * (c * c)) / total_mass));
-    float xacc = cart_in - ((pml * th_acc) * c) / total_mass;
+    S uu = vclamp(u[0], -100.0f, 100.0f);
+    S x = s_[0], dx = s_[1], c = s_[2], s = s_[3], dth = s_[4];
+    S th = vatan2(s, c);
+    S cart_in = (uu + (pml * (dth * dth)) * s) / total_mass;
+    S th_acc = (g * s - c * cart_in) / (l * (4.0f / 3.0f - (mp * (c * c)) / total_mass));
+    S xacc = cart_in - ((pml * th_acc) * c) / total_mass;
     o[0] = x + DT * dx;
     o[1] = dx + DT * xacc;
-    float th2 = th + DT * dth;
-    o[2] = cosf(th2);
-    o[3] = sinf(th2);
+    S th2 = th + DT * dth;
+    vsincos(th2, o[3], o[2]);
     o[4] = dth + DT * th_acc;
   }
 
@@ -106,7 +107,9 @@ struct Cartpole {
   // cartpole.py:790-839 (closed form of the same derivative)
   DEV void jacobian(const float (&s_)[N], const float (&u)[M], float (&D)[N][N + M]) const {
     const float th2 = next_angle(s_[2], s_[3], s_[4]);
-    jacobian_sc(s_, u, cosf(th2), sinf(th2), D);
+    float sn, cs;
+    vsincos(th2, sn, cs);
+    jacobian_sc(s_, u, cs, sn, D);
   }
 
   // The Jacobian's cos/sin of the integrated angle are exactly components 2 and
