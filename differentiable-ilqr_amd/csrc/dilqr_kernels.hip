@@ -12,6 +12,7 @@ namespace dilqr {
 
 constexpr int kBlock = 64;   // one wave per workgroup: 64 problems, 4 workgroups per CU
                              // at B=65536, freely distributed over the 8 XCDs.
+constexpr size_t kLdsPerCU = 160 * 1024;   // CDNA4 LDS per CU
 
 static inline int grid_for(long long n) { return (int)((n + kBlock - 1) / kBlock); }
 
@@ -721,15 +722,24 @@ struct SweepIn {
   }
 };
 
+// Where the fused iteration keeps its gain records (K_t, k_t), written by the
+// sweep and read back by the line search: a float4-column workspace in HBM
+// (stride B, index b), or the workgroup's LDS (stride 64, index = lane) — each
+// lane reads only what it wrote, so no barrier is involved.
+struct GainRecs {
+  float* p;
+  int B, b;
+};
+
 template <int n, int m, int GREC, bool SOA, int BM>
 struct FwdIn {
   static constexpr int d = n + m;
   float g[GREC], u[m], C[d][d], c[d], xnext[n];
   StepBounds<m, BM> bnd;
   template <class CostT>
-  DEV void load(const float* __restrict__ grec, const float* __restrict__ up, const CostT& cs,
+  DEV void load(const GainRecs& gr, const float* __restrict__ up, const CostT& cs,
                 const float* __restrict__ xp, const Bounds& bd, int T, int t, int t1, int B, int b) {
-    SoaRec<GREC>::load(g, grec, T, t, B, b); ld_traj<SOA>(u, up, t, B, b); cs.load(C, c, t, B, b);
+    SoaRec<GREC>::load(g, gr.p, T, t, gr.B, gr.b); ld_traj<SOA>(u, up, t, B, b); cs.load(C, c, t, B, b);
     ld_traj<SOA>(xnext, xp, t1, B, b); bnd.load(bd, t, B, b);
   }
 };
@@ -752,7 +762,7 @@ constexpr int kPF = DILQR_PF;
 template <class Model, int BM, bool SOA, class CostT>
 DEV int line_search(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
                     const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd, float decay,
-                    int max_ls, const float* __restrict__ ws, float* __restrict__ xa_out,
+                    int max_ls, const GainRecs& ws, float* __restrict__ xa_out,
                     float* __restrict__ ua_out, float* __restrict__ xb_out, float* __restrict__ ub_out,
                     float* __restrict__ du_sq, float old_cost, float& cost_out, float& alpha_out) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
@@ -859,7 +869,7 @@ template <class Model, int BM, bool SOA, bool ROLLOUT, class CostT>
 DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
                      float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
-                     float* __restrict__ ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
+                     const GainRecs& ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
                      float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
                      float& cost_out, float& alpha_out) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
@@ -944,7 +954,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
         for (int j = 0; j < n; ++j) g[a * n + j] = Kt[a][j];
         g[m * n + a] = kt[a];
       }
-      SoaRec<GREC>::store(ws, g, T, t, B, b);
+      SoaRec<GREC>::store(ws.p, g, T, t, ws.B, ws.b);
       old_cost += obj;          // summed over t = T-1..0 (the reference's torch sum has its own order)
 #pragma unroll
       for (int i = 0; i < n; ++i) xn[i] = cur.x[i];
@@ -990,7 +1000,7 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
   float* ub = xb + (size_t)T * B * n;
   const int win = ilqr_problem<Model, BM, false, false>(T, B, b, md, x_init, CostFull<n + m>{C, c}, nullptr, nullptr, x, u,
                                                    bd, decay,
-                                            max_ls, ws,
+                                            max_ls, GainRecs{ws, B, b},
                                             x_out, u_out, xb, ub, du_sq, cost, alpha);
   if (win) {
     for (int t = 0; t < T; ++t) {
@@ -1028,7 +1038,10 @@ DEV void free_slots(int cur, int best, int& sa, int& sb) {
   }
 }
 
-template <class Model, int BM>
+// LG: the gain records live in this workgroup's LDS (dynamic, T*64*GREC floats;
+// dilqr_mpc_step_f32 picks it when 4 workgroups per CU still fit the 160 KB),
+// instead of a workspace round trip through HBM/MALL every iteration.
+template <class Model, int BM, bool LG>
 __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const float* __restrict__ theta,
                                                         const float* __restrict__ x_init, const float* __restrict__ C,
                                                         const float* __restrict__ c, Bounds bd, float decay, int max_ls,
@@ -1046,6 +1059,8 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   free_slots(cur, best, sa, sb);
   float cost, alpha;
   int win;
+  extern __shared__ __attribute__((aligned(16))) float lds_gains[];
+  const GainRecs gr = LG ? GainRecs{lds_gains, kBlock, (int)threadIdx.x} : GainRecs{S.ws, B, b};
   // the solve's packed symmetric cost: built by iteration 0's sweep (which reads
   // C, c), used from iteration 1 on by every problem whose C_t are all bitwise
   // symmetric, reading only diag(C_t) and c_t when they are all diagonal too
@@ -1057,7 +1072,7 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
       CostDiagConst<n + m> cc;
       cc.init(S.Cpk, T, B, b);
       win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, cc, nullptr, nullptr, S.Xs + cur * TBn,
-                                                S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn,
+                                                S.Us + cur * TBm, bd, decay, max_ls, gr, S.Xs + sa * TBn,
                                                 S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost,
                                                 alpha);
     } else {
@@ -1066,24 +1081,24 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   } else if (pk & kCostDiag) {           // set by iteration 0 only when packed_diag_ok
     if constexpr (packed_diag_ok<n + m>())
       win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr, nullptr,
-                                          S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws,
+                                          S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, gr,
                                           S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm,
                                           S.du_sq, cost, alpha);
     else
       __builtin_unreachable();
   } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
     win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T}, nullptr,
-                                    nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws,
+                                    nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, gr,
                                     S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq,
                                     cost, alpha);
   else if (pk & kCostSym)
     win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
-                                    S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, S.ws, S.Xs + sa * TBn,
+                                    S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, gr, S.Xs + sa * TBn,
                                     S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost, alpha);
   else
     win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
                                     first && S.Cpk ? S.cost_sym : nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd,
-                                    decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
+                                    decay, max_ls, gr, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
                                     S.Us + sb * TBm, S.du_sq, cost, alpha);
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
@@ -2291,9 +2306,17 @@ int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float*
           G, st);
   } else {
 #define LAUNCH_MPC(BM_)                                                                                      \
-  k_mpc_iterate<MD, BM_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, theta, x_init, C, c, bd, linesearch_decay, \
-                                                               max_linesearch_iter, iteration, best_cost_eps, eps, \
-                                                               lim, G, st)
+  do {                                                                                                       \
+    const size_t lds = (size_t)T * kBlock * (MD::N * MD::M + MD::M) * sizeof(float);                        \
+    if (lds * 4 <= kLdsPerCU)                                                                                \
+      k_mpc_iterate<MD, BM_, true><<<grid_for(B), kBlock, lds, S(stream)>>>(                                 \
+          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, \
+          lim, G, st);                                                                                       \
+    else                                                                                                     \
+      k_mpc_iterate<MD, BM_, false><<<grid_for(B), kBlock, 0, S(stream)>>>(                                  \
+          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, \
+          lim, G, st);                                                                                       \
+  } while (0)
     MODEL_SWITCH_TPP(model, ({
       if (bounds.mode == DILQR_BOUNDS_TENSOR) LAUNCH_MPC(DILQR_BOUNDS_TENSOR);
       else if (box) LAUNCH_MPC(DILQR_BOUNDS_SCALAR);
