@@ -37,9 +37,30 @@ N_STATE, N_CTRL = 5, 1
 D = N_STATE + N_CTRL
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 
-# Algorithmic bytes, fp32:
-#  fused iteration, per problem: C, c, x_init, tau in / tau out, cost, du_norm
-ITER_BYTES_PER_PROBLEM = 4 * (T_HORIZON * D * D + T_HORIZON * D + N_STATE + 2 * T_HORIZON * D + 2)   # 5,428
+# Algorithmic bytes, fp32.
+#  Fused MPC iteration, per problem: the stage cost AS THE TIMED PATH READS IT
+#  (iter_cost_floats), x_init, the current trajectory in, the new one out,
+#  cost and du_norm.  SURVEY.md's 5,428 B/problem counts the caller's C, c at
+#  every step; the kernel reads the solve's packed copy instead, and for the
+#  reference's own cost (diag(q), p repeated over t) only its 2d floats once.
+PACKED_FLOATS = D * (D + 1) // 2 + D                                   # 27 at d=6
+
+
+def iter_cost_floats(flags, T=T_HORIZON, d=D):
+    """Cost floats one iteration (>= 1) reads per problem, by the iteration-0
+    flags (dilqr.h dilqr_mpc_state: bit0 symmetric, bit1 diagonal, bit2 time-invariant)."""
+    pk = d * (d + 1) // 2 + d
+    f = np.asarray(flags).astype(np.int64)
+    out = np.full(f.shape, T * (d * d + d), np.float64)                    # asymmetric: the caller's C, c
+    out[(f & 1) != 0] = T * pk                                              # packed symmetric
+    out[(f & 5) == 5] = pk                                                  # ... time-invariant: one record
+    out[(f & 3) == 3] = T * 2 * d                                           # diagonal: diag(C_t), c_t
+    out[(f & 7) == 7] = 2 * d                                               # ... time-invariant: in registers
+    return out
+
+
+def iter_bytes_per_problem(cost_floats, T=T_HORIZON, n=N_STATE, d=D):
+    return 4 * (cost_floats + n + 2 * T * d + 2)
 #  Riccati sweep, per problem: C, c_back, F in; K, k out
 SWEEP_BYTES_PER_PROBLEM = 4 * (T_HORIZON * D * D + T_HORIZON * D + (T_HORIZON - 1) * N_STATE * D
                                + T_HORIZON * N_CTRL * N_STATE + T_HORIZON * N_CTRL)                  # 7,680
@@ -142,6 +163,49 @@ def sweep_roofline(n, m, T, B, dev, reps=5):
     gbs = nbytes / (ms * 1e-3) / 1e9
     return {"shape": [n, m, T, B], "avg_launch_ms": ms, "algorithmic_bytes_per_launch": nbytes,
             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}
+
+
+def dense_cost_roofline(dev, x0, theta, B, reps=10):
+    """The same fused iteration on a cost that really streams: a dense SPD C_t,b
+    distinct per (t, b) (bitwise symmetric, so the packed-symmetric path: 27
+    floats per step), iterations 1..reps timed with HIP events on the launch
+    stream.  Bytes per problem: 4*(T*27 + n + 2*T*d + 2) = 3,928."""
+    from dilqr import _native as N
+    from dilqr import ops
+    T = T_HORIZON
+    g = torch.Generator(device=dev).manual_seed(5)
+    L = torch.randn(T, B, D, D, device=dev, generator=g) * (0.3 / D ** 0.5)
+    A = L @ L.transpose(-1, -2)
+    del L
+    q = torch.tensor([0.1, 0.1, 1., 1., 0.1, 0.001], device=dev)
+    C = (0.5 * (A + A.transpose(-1, -2)) + torch.diag(q)).contiguous()   # bitwise symmetric
+    del A
+    c = (torch.tensor([0., 0., -1., 0., 0., 0.], device=dev) + 0.01 * torch.randn(T, B, D, device=dev, generator=g))
+    c = c.contiguous()
+    sv = ops.MPCSolve(T, B, N_STATE, N_CTRL, dev)
+    nb, _ = N.make_bounds(None, None)
+    s = N.stream(dev)
+    stream = torch.cuda.current_stream(dev)
+    sv.begin(N.MODEL_CARTPOLE, theta, x0)
+    sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for r in range(reps):
+        ev[r][0].record(stream)
+        N.call("dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T, B, N.ptr(theta), N.ptr(x0), N.ptr(C), N.ptr(c), nb, 0.5,
+               2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s)
+        ev[r][1].record(stream)
+        N.call("dilqr_mpc_stop_rule_f32", T, N_CTRL, B, r + 1, sv.state, s)
+    torch.cuda.synchronize(dev)
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    cf = iter_cost_floats(sv.cost_sym.cpu().numpy())
+    nbytes = float(iter_bytes_per_problem(cf).sum())
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    del sv, C, c
+    return {"kernel": "k_mpc_iterate<Cartpole,UNC,LDS gains> (packed symmetric cost, 27 floats per step)",
+            "workload": "dense SPD C_t,b distinct per (t,b), cartpole T=25, 65536 problems",
+            "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": ms,
+            "problem_iters_per_s": B / (ms * 1e-3)}
 
 
 def secondary_configs(dev):
@@ -353,7 +417,10 @@ def main():
         N.call("dilqr_mpc_stop_rule_f32", T_HORIZON, N_CTRL, B, r + 1, sv.state, s)
     torch.cuda.synchronize(dev)
     iter_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    iter_bytes = ITER_BYTES_PER_PROBLEM * B
+    cost_floats = iter_cost_floats(sv.cost_sym.cpu().numpy())
+    iter_bytes = float(iter_bytes_per_problem(cost_floats).sum())
+    cost_path = ("time-invariant diagonal cost held in registers (2d floats per problem)"
+                 if (cost_floats == 2 * D).all() else f"mixed cost paths, {cost_floats.mean():.0f} cost floats/problem")
     xa, ua = sv.gather_best()
 
     # standalone Riccati sweep (the north-star's >=50% HBM target kernel)
@@ -372,14 +439,20 @@ def main():
     sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in sev]))
     sweep_bytes = SWEEP_BYTES_PER_PROBLEM * B
 
-    traffic = None
+    # PMC figures of the same kernel at this shape (tools/profile_pmc.sh over
+    # `bench.py --kernels-only`, summarised by tools/pmc_summary.py): L2-miss
+    # bytes per launch with calibrated counter factors, raw counters, and the
+    # issue breakdown (what bounds the kernel: VALU issue, not HBM)
+    traffic, pmc = None, {}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmc_path)).get("k_mpc_iterate_bytes_per_launch")
+            pmc = json.load(open(pmc_path))
+            traffic = pmc.get("k_mpc_iterate_bytes_per_launch")
             traffic = None if traffic is None else traffic * B / B_PER_GPU
         except Exception:
-            traffic = None
+            traffic, pmc = None, {}
+    dense = None if args.kernels_only or world > 1 else dense_cost_roofline(dev, x0, theta, B)
 
     if rank == 0 and args.kernels_only:
         print(json.dumps({"iter_ms": iter_ms, "sweep_ms": sweep_ms}), flush=True)
@@ -406,11 +479,16 @@ def main():
                        "batch_per_gpu": B, "global_batch": B_total, "T": T_HORIZON,
                        "parallelism": f"batch-sharded x{world} (no collective)",
                        "batch_iters_per_s": world * args.steps / elapsed},
-            "roofline": {"kernel": "k_mpc_iterate<Cartpole,UNC> (fused linearise+Riccati+line search, "
-                                   "packed symmetric cost)",
+            "roofline": {"kernel": "k_mpc_iterate<Cartpole,UNC,LDS gains> (fused linearise+Riccati+line search; "
+                                   + cost_path + ")",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": iter_bytes, "avg_launch_ms": iter_ms},
+                         "traffic_raw_KiB": pmc.get("k_mpc_iterate_raw"),
+                         "traffic_measured_at": pmc.get("measured_at_commit"),
+                         "algorithmic_bytes_per_launch": iter_bytes, "avg_launch_ms": iter_ms,
+                         "limiter": {"what": "VALU issue at one wave per SIMD (B=65536 = 1024 waves); not HBM",
+                                     **(pmc.get("k_mpc_iterate_issue") or {})}},
+            "roofline_dense_cost": dense,
             "riccati_roofline": {"kernel": "k_lqr_backward<5,1,UNC> (standalone sweep, F from HBM)",
                                  "bound": "hbm", "achieved": sweep_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": sweep_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": sweep_bytes,
