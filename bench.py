@@ -399,7 +399,7 @@ def main():
         tt = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    assert bool(torch.isfinite(sv.best_cost).all()), "non-finite costs"
+    assert args.kernels_only or bool(torch.isfinite(sv.best_cost).all()), "non-finite costs"
 
     # ---- roofline of the dominant kernel: the fused MPC iteration kernel
     # (k_mpc_iterate), timed with HIP events on ITS stream (the current stream,

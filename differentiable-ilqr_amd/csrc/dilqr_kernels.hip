@@ -471,48 +471,19 @@ __global__ void __launch_bounds__(kBlock) k_pnqp(int B, const float* __restrict_
 // ============================================================ fused iLQR iteration
 // One MPC iteration body (mpc_explicit.py:249-263) for ONE problem (this lane):
 // linearise at the current trajectory on the fly, Riccati sweep (+pnqp), the
-// current cost, and the line-search rollout.  F never touches HBM; K/k/obj_t go
-// to a per-lane record that the rollout re-reads (L2/MALL-hot).
+// current cost, and the line-search rollout.  F never touches HBM; K/k go to
+// per-lane gain records (LDS in the MPC kernel) that the rollout re-reads.
 //
 // Latency: at B=65536 there is one wave per SIMD, so every loop software-
-// pipelines its HBM loads one step ahead in registers (the step t-1 / t+1
-// record is in flight while step t computes).
-// Private workspaces are component-major ("SoA"): element j of record (t,b) is
-// at [(t*K + j)*B + b], so a wave's 64 lanes touch 64 consecutive words per
-// access (one fully used 256-B run) instead of 64 records K words apart.  For
-// stores this doubles the rate (tools/microbench/store_patterns.hip: 112-B
-// records per lane 3.3 TB/s, coalesced 6.6 TB/s); loads lose little either way.
-// The MPC trajectory slots of the thread-per-problem models use it too
-// ([slot][T][n][B]); the caller's tensors keep the reference layout ("AoS").
-template <int K>
-DEV void ld_soa(float (&r)[K], const float* __restrict__ p, size_t t, int B, int b) {
-#pragma unroll
-  for (int i = 0; i < K; ++i) r[i] = p[(t * K + i) * B + b];
-}
-template <int K>
-DEV void st_soa(float* __restrict__ p, const float (&r)[K], size_t t, int B, int b) {
-#pragma unroll
-  for (int i = 0; i < K; ++i) p[(t * K + i) * B + b] = r[i];
-}
-// records of K floats (K % 4 == 0) as float4 columns: [(t*K/4 + j)*B + b]
-template <int K>
-DEV void ld_soa4(float (&r)[K], const float* __restrict__ p, size_t t, int B, int b) {
-  static_assert(K % 4 == 0, "");
-  const float4* q = reinterpret_cast<const float4*>(p);
-#pragma unroll
-  for (int j = 0; j < K / 4; ++j) {
-    float4 v = q[(t * (K / 4) + j) * B + b];
-    r[4 * j] = v.x; r[4 * j + 1] = v.y; r[4 * j + 2] = v.z; r[4 * j + 3] = v.w;
-  }
-}
-template <int K>
-DEV void st_soa4(float* __restrict__ p, const float (&r)[K], size_t t, int B, int b) {
-  static_assert(K % 4 == 0, "");
-  float4* q = reinterpret_cast<float4*>(p);
-#pragma unroll
-  for (int j = 0; j < K / 4; ++j) q[(t * (K / 4) + j) * B + b] = make_float4(r[4 * j], r[4 * j + 1], r[4 * j + 2], r[4 * j + 3]);
-}
-
+// pipelines its loads one step ahead in registers (the step t-1 / t+1 inputs
+// are in flight while step t computes).
+// Private workspaces of per-(t,b) values the kernel re-reads column by column
+// (gain records in HBM, the packed cost copy) are component-major: element j
+// of record (t,b) is at [(t*K + j)*B + b] in float4/float2/float planes, so a
+// wave's 64 lanes touch one contiguous run per access.  The MPC trajectory
+// slots hold whole [x_t; u_t] records per lane instead (TRAJ_REC, below):
+// fewer, wider accesses where the count of memory instructions, not bytes,
+// is what the one-wave-per-SIMD kernel pays for.
 // records of K floats stored as column planes of the widest vector loads:
 // K/4 float4 planes, then a float2 plane if K%4 >= 2, then a float plane if K
 // is odd (plane q of width w: w*[(t*nq + q)*B + b] floats from its base).
@@ -545,16 +516,48 @@ struct SoaRec {
   }
 };
 
-// trajectories: the caller's [T,B,K] (SOA=false) or the slots' [T,K,B]
-template <bool SOA, int K>
-DEV void ld_traj(float (&r)[K], const float* __restrict__ p, size_t t, int B, int b) {
-  if constexpr (SOA) ld_soa<K>(r, p, t, B, b);
-  else ld(r, p + (t * B + b) * K);
+// Trajectory layouts of the fused kernels:
+//  TRAJ_AOS — the caller's x [T,B,n] and u [T,B,m] (the reference's layout);
+//  TRAJ_REC — the MPC slots of the thread-per-problem models: one record
+//    [x_t; u_t] of d = n+m floats per (t, b), [T,B,d].  A lane moves its
+//    record with two wide accesses (cartpole: dwordx4 + dwordx2) instead of d
+//    dword accesses; the line search stores record t of each candidate once
+//    both x_t and u_t are known.  (The earlier component-major slots took 13
+//    dword stores per line-search step.)
+constexpr int TRAJ_AOS = 0, TRAJ_REC = 1;
+
+template <int TL, int n, int m>
+DEV void ld_xu(float (&x)[n], float (&u)[m], const float* __restrict__ xp, const float* __restrict__ up, size_t t,
+               int B, int b) {
+  const size_t tb = t * B + b;
+  if constexpr (TL == TRAJ_REC) {
+    float r[n + m];
+    ld(r, xp + tb * (n + m));
+#pragma unroll
+    for (int i = 0; i < n; ++i) x[i] = r[i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) u[a] = r[n + a];
+  } else {
+    ld(x, xp + tb * n);
+    ld(u, up + tb * m);
+  }
 }
-template <bool SOA, int K>
-DEV void st_traj(float* __restrict__ p, const float (&r)[K], size_t t, int B, int b) {
-  if constexpr (SOA) st_soa<K>(p, r, t, B, b);
-  else st(p + (t * B + b) * K, r);
+
+template <int TL, int n, int m>
+DEV void st_xu(float* __restrict__ xp, float* __restrict__ up, const float (&x)[n], const float (&u)[m], size_t t,
+               int B, int b) {
+  const size_t tb = t * B + b;
+  if constexpr (TL == TRAJ_REC) {
+    float r[n + m];
+#pragma unroll
+    for (int i = 0; i < n; ++i) r[i] = x[i];
+#pragma unroll
+    for (int a = 0; a < m; ++a) r[n + a] = u[a];
+    st(xp + tb * (n + m), r);
+  } else {
+    st(xp + tb * n, x);
+    st(up + tb * m, u);
+  }
 }
 
 // Where the fused kernels read the stage cost from: the caller's C [T,B,d,d] and
@@ -710,7 +713,7 @@ struct StepBounds {
   }
 };
 
-template <int n, int m, bool SOA, int BM>
+template <int n, int m, int TL, int BM>
 struct SweepIn {
   static constexpr int d = n + m;
   float C[d][d], c[d], x[n], u[m];
@@ -718,7 +721,7 @@ struct SweepIn {
   template <class CostT>
   DEV void load(const CostT& cs, const float* __restrict__ xp, const float* __restrict__ up, const Bounds& bd, int t,
                 int B, int b) {
-    cs.load(C, c, t, B, b); ld_traj<SOA>(x, xp, t, B, b); ld_traj<SOA>(u, up, t, B, b); bnd.load(bd, t, B, b);
+    cs.load(C, c, t, B, b); ld_xu<TL>(x, u, xp, up, t, B, b); bnd.load(bd, t, B, b);
   }
 };
 
@@ -731,16 +734,25 @@ struct GainRecs {
   int B, b;
 };
 
-template <int n, int m, int GREC, bool SOA, int BM>
+// Inputs of line-search step t: gains, u_t and x_{t+1} of the current
+// trajectory, the stage cost, bounds.  TRAJ_REC reads record t+1 whole (x_{t+1}
+// and u_{t+1}); u_t is carried over from the previous step's record (the
+// caller sets `u` of step 0 and copies `unext` forward).
+template <int n, int m, int GREC, int TL, int BM>
 struct FwdIn {
   static constexpr int d = n + m;
-  float g[GREC], u[m], C[d][d], c[d], xnext[n];
+  float g[GREC], u[m], C[d][d], c[d], xnext[n], unext[m];
   StepBounds<m, BM> bnd;
   template <class CostT>
   DEV void load(const GainRecs& gr, const float* __restrict__ up, const CostT& cs,
                 const float* __restrict__ xp, const Bounds& bd, int T, int t, int t1, int B, int b) {
-    SoaRec<GREC>::load(g, gr.p, T, t, gr.B, gr.b); ld_traj<SOA>(u, up, t, B, b); cs.load(C, c, t, B, b);
-    ld_traj<SOA>(xnext, xp, t1, B, b); bnd.load(bd, t, B, b);
+    SoaRec<GREC>::load(g, gr.p, T, t, gr.B, gr.b); cs.load(C, c, t, B, b); bnd.load(bd, t, B, b);
+    if constexpr (TL == TRAJ_REC) {
+      ld_xu<TL>(xnext, unext, xp, up, t1, B, b);
+    } else {
+      ld(u, up + ((size_t)t * B + b) * m);
+      ld(xnext, xp + ((size_t)t1 * B + b) * n);
+    }
   }
 };
 
@@ -759,7 +771,7 @@ constexpr int kPF = DILQR_PF;
 // and B), sharing every load of the step; the first accepted candidate wins,
 // which is exactly the sequential search.  A wave otherwise pays a whole
 // second latency-bound pass whenever any of its 64 problems backtracks.
-template <class Model, int BM, bool SOA, class CostT>
+template <class Model, int BM, int TL, class CostT>
 DEV int line_search(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
                     const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd, float decay,
                     int max_ls, const GainRecs& ws, float* __restrict__ xa_out,
@@ -785,14 +797,20 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
       ld(x0, x_init + (size_t)b * n);
 #pragma unroll
       for (int i = 0; i < n; ++i) { xp[i] = f2{x0[i], x0[i]}; dp[i] = f2{0.f, 0.f}; }
-      st_traj<SOA>(xa_out, x0, 0, B, b);
-      if (twoB) st_traj<SOA>(xb_out, x0, 0, B, b);
+      if constexpr (TL == TRAJ_AOS) {
+        st(xa_out + (size_t)b * n, x0);
+        if (twoB) st(xb_out + (size_t)b * n, x0);
+      }
     }
     f2 cp = {0.f, 0.f};
     // step s's record holds x_{s+1} of the current trajectory; indices clamp at T-1
     auto cl = [T](int s) { return s < T ? s : T - 1; };
-    FwdIn<n, m, GREC, SOA, BM> cur, n1, n2;
+    FwdIn<n, m, GREC, TL, BM> cur, n1, n2;
     cur.load(ws, u, cs, x, bd, T, 0, cl(1), B, b);
+    if constexpr (TL == TRAJ_REC) {                     // u_0 from record 0
+      float x0r[n];
+      ld_xu<TL>(x0r, cur.u, x, u, 0, B, b);
+    }
     if constexpr (kPF >= 2) n1.load(ws, u, cs, x, bd, T, cl(1), cl(2), B, b);
     for (int t = 0; t < T; ++t) {
       if constexpr (kPF >= 2) n2.load(ws, u, cs, x, bd, T, cl(t + 2), cl(t + 3), B, b);   // prefetch step t+2
@@ -813,8 +831,16 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
         float ua[m], ub[m];
 #pragma unroll
         for (int a = 0; a < m; ++a) { ua[a] = nu[a].x; ub[a] = nu[a].y; }
-        st_traj<SOA>(ua_out, ua, t, B, b);
-        if (twoB) st_traj<SOA>(ub_out, ub, t, B, b);
+        if constexpr (TL == TRAJ_REC) {               // record t of each candidate: x_t, u_t
+          float xa[n], xb[n];
+#pragma unroll
+          for (int i = 0; i < n; ++i) { xa[i] = xp[i].x; xb[i] = xp[i].y; }
+          st_xu<TL>(xa_out, nullptr, xa, ua, t, B, b);
+          if (twoB) st_xu<TL>(xb_out, nullptr, xb, ub, t, B, b);
+        } else {
+          st(ua_out + ((size_t)t * B + b) * m, ua);
+          if (twoB) st(ub_out + ((size_t)t * B + b) * m, ub);
+        }
       }
       if (p == 0) {
 #pragma unroll
@@ -840,8 +866,14 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
           xa[i] = xnext[i].x;
           xb[i] = xnext[i].y;
         }
-        st_traj<SOA>(xa_out, xa, t + 1, B, b);
-        if (twoB) st_traj<SOA>(xb_out, xb, t + 1, B, b);
+        if constexpr (TL == TRAJ_AOS) {
+          st(xa_out + ((size_t)(t + 1) * B + b) * n, xa);
+          if (twoB) st(xb_out + ((size_t)(t + 1) * B + b) * n, xb);
+        }
+      }
+      if constexpr (TL == TRAJ_REC) {
+#pragma unroll
+        for (int a = 0; a < m; ++a) n1.u[a] = cur.unext[a];     // u_{t+1}
       }
       cur = n1;
       if constexpr (kPF >= 2) n1 = n2;
@@ -856,7 +888,7 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
   return win;
 }
 
-// x, u (current trajectory) and the candidate outputs in layout SOA; the gain
+// x, u (current trajectory) and the candidate outputs in layout TL; the gain
 // records in ws and the packed cost are always float4-column.  ROLLOUT: x is a
 // rollout of the model under u (the MPC slots are), so x_{t+1} = forward(x_t,
 // u_t) bit for bit and models with kJacFromNext take part of the Jacobian from it.
@@ -865,7 +897,7 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
 // records a later change of the cost proves necessary are written then, from
 // the registers holding that record), and a time-invariant diagonal cost is
 // handed to this iteration's line search in registers, so C is read once.
-template <class Model, int BM, bool SOA, bool ROLLOUT, class CostT>
+template <class Model, int BM, int TL, bool ROLLOUT, class CostT>
 DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
                      float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
@@ -888,7 +920,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
 #pragma unroll
     for (int i = 0; i < n; ++i) xn[i] = 0.f;
     // inputs of step t, t-1 (and t-2 at kPF = 2) in flight together
-    SweepIn<n, m, SOA, BM> cur, n1, n2;
+    SweepIn<n, m, TL, BM> cur, n1, n2;
     cur.load(cs, x, u, bd, T - 1, B, b);
     if constexpr (kPF >= 2) n1.load(cs, x, u, bd, T > 1 ? T - 2 : 0, B, b);
     for (int t = T - 1; t >= 0; --t) {
@@ -970,11 +1002,11 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     if (pack_out && sym && diag && tinv) {              // iteration 0 of a diag(q), p over t cost
       CostDiagConst<d> cc;
       cc.set(pk_last);
-      return line_search<Model, BM, SOA>(T, B, b, md, x_init, cc, x, u, bd, decay, max_ls, ws, xa_out, ua_out,
+      return line_search<Model, BM, TL>(T, B, b, md, x_init, cc, x, u, bd, decay, max_ls, ws, xa_out, ua_out,
                                          xb_out, ub_out, du_sq, old_cost, cost_out, alpha_out);
     }
   }
-  return line_search<Model, BM, SOA>(T, B, b, md, x_init, cs, x, u, bd, decay, max_ls, ws, xa_out, ua_out, xb_out,
+  return line_search<Model, BM, TL>(T, B, b, md, x_init, cs, x, u, bd, decay, max_ls, ws, xa_out, ua_out, xb_out,
                                      ub_out, du_sq, old_cost, cost_out, alpha_out);
 }
 
@@ -998,7 +1030,7 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
   // over (x_out, u_out) when it wins
   float* xb = ws + (size_t)T * B * GREC;
   float* ub = xb + (size_t)T * B * n;
-  const int win = ilqr_problem<Model, BM, false, false>(T, B, b, md, x_init, CostFull<n + m>{C, c}, nullptr, nullptr, x, u,
+  const int win = ilqr_problem<Model, BM, TRAJ_AOS, false>(T, B, b, md, x_init, CostFull<n + m>{C, c}, nullptr, nullptr, x, u,
                                                    bd, decay,
                                             max_ls, GainRecs{ws, B, b},
                                             x_out, u_out, xb, ub, du_sq, cost, alpha);
@@ -1053,10 +1085,13 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   Model md; md.load(theta);
-  const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
+  const size_t TBd = (size_t)T * B * (n + m);               // one slot: [T,B,d] records
   const int cur = S.slot[b], best = S.slot[B + b];
   int sa, sb;
   free_slots(cur, best, sa, sb);
+  const float* xcur = S.Xs + cur * TBd;
+  float* xsa = S.Xs + sa * TBd;
+  float* xsb = S.Xs + sb * TBd;
   float cost, alpha;
   int win;
   extern __shared__ __attribute__((aligned(16))) float lds_gains[];
@@ -1071,35 +1106,31 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
     if constexpr (packed_diag_ok<n + m>()) {
       CostDiagConst<n + m> cc;
       cc.init(S.Cpk, T, B, b);
-      win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, cc, nullptr, nullptr, S.Xs + cur * TBn,
-                                                S.Us + cur * TBm, bd, decay, max_ls, gr, S.Xs + sa * TBn,
-                                                S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost,
+      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
                                                 alpha);
     } else {
       __builtin_unreachable();
     }
   } else if (pk & kCostDiag) {           // set by iteration 0 only when packed_diag_ok
     if constexpr (packed_diag_ok<n + m>())
-      win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr, nullptr,
-                                          S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, gr,
-                                          S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm,
+      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr, nullptr,
+                                          xcur, nullptr, bd, decay, max_ls, gr,
+                                          xsa, nullptr, xsb, nullptr,
                                           S.du_sq, cost, alpha);
     else
       __builtin_unreachable();
   } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
-    win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T}, nullptr,
-                                    nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, gr,
-                                    S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq,
+    win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T}, nullptr,
+                                    nullptr, xcur, nullptr, bd, decay, max_ls, gr,
+                                    xsa, nullptr, xsb, nullptr, S.du_sq,
                                     cost, alpha);
   else if (pk & kCostSym)
-    win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
-                                    S.Xs + cur * TBn, S.Us + cur * TBm, bd, decay, max_ls, gr, S.Xs + sa * TBn,
-                                    S.Us + sa * TBm, S.Xs + sb * TBn, S.Us + sb * TBm, S.du_sq, cost, alpha);
+    win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
+                                    xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost, alpha);
   else
-    win = ilqr_problem<Model, BM, true, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
-                                    first && S.Cpk ? S.cost_sym : nullptr, S.Xs + cur * TBn, S.Us + cur * TBm, bd,
-                                    decay, max_ls, gr, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
-                                    S.Us + sb * TBm, S.du_sq, cost, alpha);
+    win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
+                                    first && S.Cpk ? S.cost_sym : nullptr, xcur, nullptr, bd,
+                                    decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost, alpha);
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
   S.alpha[b] = alpha;
@@ -1290,13 +1321,15 @@ DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_i
   return out.stopped != 0;
 }
 
-// slot layout: component-major for the thread-per-problem models, the
-// caller's [T,B,k] for the 16-lanes-per-problem ones
+// slot layout: [T,B,d] records for the thread-per-problem models (TRAJ_REC;
+// the state's Us is unused), the caller's [T,B,n] / [T,B,m] for the
+// 16-lanes-per-problem ones
 template <class Model>
-constexpr bool soa_slots() { return Model::N + Model::M <= 8; }
-constexpr bool soa_slots_nm(int n, int m) { return n + m <= 8; }
+constexpr int slot_layout() { return Model::N + Model::M <= 8 ? TRAJ_REC : TRAJ_AOS; }
+constexpr int slot_layout_nm(int n, int m) { return n + m <= 8 ? TRAJ_REC : TRAJ_AOS; }
 
-// rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl.
+// rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl.  The
+// caller has placed u_init (or zeros) in slot 0's u.
 template <class Model>
 __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float* __restrict__ theta,
                                                       const float* __restrict__ x_init, MpcState S) {
@@ -1312,17 +1345,18 @@ __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float*
   if (b >= B) return;
   Model md; md.load(theta);
   S.slot[b] = 0; S.slot[B + b] = 0;
-  constexpr bool SOA = soa_slots<Model>();
+  constexpr int TL = slot_layout<Model>();
   float xt[n];
   ld(xt, x_init + (size_t)b * n);
-  st_traj<SOA>(S.Xs, xt, 0, B, b);
-  for (int t = 0; t < T - 1; ++t) {
-    float ut[m], xn[n];
-    ld_traj<SOA>(ut, S.Us, t, B, b);
-    md.forward(xt, ut, xn);
+  for (int t = 0; t < T; ++t) {
+    float ut[m], xo[n], xn[n];
+    ld_xu<TL>(xo, ut, S.Xs, S.Us, t, B, b);
+    st_xu<TL>(S.Xs, S.Us, xt, ut, t, B, b);
+    if (t < T - 1) {
+      md.forward(xt, ut, xn);
 #pragma unroll
-    for (int i = 0; i < n; ++i) xt[i] = xn[i];
-    st_traj<SOA>(S.Xs, xt, t + 1, B, b);
+      for (int i = 0; i < n; ++i) xt[i] = xn[i];
+    }
   }
 }
 
@@ -1332,13 +1366,13 @@ __global__ void __launch_bounds__(kBlock) k_mpc_gather(int T, int B, MpcState S,
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   int best = S.slot[B + b];
-  constexpr bool SOA = soa_slots_nm(n, m);
-  const float* X = S.Xs + (size_t)best * T * B * n;
+  constexpr int TL = slot_layout_nm(n, m);
+  const float* X = S.Xs + (size_t)best * T * B * (TL == TRAJ_REC ? n + m : n);
   const float* U = S.Us + (size_t)best * T * B * m;
   for (int t = 0; t < T; ++t) {
     size_t tb = (size_t)t * B + b;
     float xt[n], ut[m];
-    ld_traj<SOA>(xt, X, t, B, b); ld_traj<SOA>(ut, U, t, B, b);
+    ld_xu<TL>(xt, ut, X, U, t, B, b);
     st(x_out + tb * n, xt); st(u_out + tb * m, ut);
   }
 }

@@ -156,11 +156,16 @@ class MPCSolve:
     def __init__(self, T, B, n, m, device, packed_cost=True):
         dev = device
         self.T, self.B, self.n, self.m = T, B, n, m
-        # slots are component-major [4,T,n,B] for the thread-per-problem models
-        # (coalesced per-lane access), the caller's [4,T,B,n] for rocket
-        self.soa = n + m <= 8
-        self.Xs = torch.empty((4, T, n, B) if self.soa else (4, T, B, n), device=dev)
-        self.Us = torch.zeros((4, T, m, B) if self.soa else (4, T, B, m), device=dev)
+        # slots: [4,T,B,n+m] records [x_t; u_t] for the thread-per-problem models
+        # (Us aliases Xs, unused by the kernels), the caller's [4,T,B,n] and
+        # [4,T,B,m] for rocket
+        self.rec = n + m <= 8
+        if self.rec:
+            self.Xs = torch.zeros((4, T, B, n + m), device=dev)
+            self.Us = self.Xs
+        else:
+            self.Xs = torch.empty((4, T, B, n), device=dev)
+            self.Us = torch.zeros((4, T, B, m), device=dev)
         self.slot = torch.zeros(2, B, dtype=torch.uint8, device=dev)
         self.best_cost = torch.empty(B, device=dev)
         self.best_du = torch.empty(B, device=dev)
@@ -184,13 +189,14 @@ class MPCSolve:
 
     def begin(self, model_id, theta, x_init, u_init=None):
         """x = get_traj(u_init or 0) into slot 0; reset slots and the control block."""
+        u_slot0 = self.Xs[0, :, :, self.n:] if self.rec else self.Us[0]
         if u_init is None:
-            self.Us[0].zero_()
+            u_slot0.zero_()
         else:
-            u0 = u_init.to(device=self.Us.device, dtype=torch.float32)
+            u0 = u_init.to(device=self.Xs.device, dtype=torch.float32)
             if u0.ndimension() == 2:
                 u0 = u0.unsqueeze(1).expand(self.T, self.B, self.m)
-            self.Us[0].copy_(u0.permute(0, 2, 1) if self.soa else u0)
+            u_slot0.copy_(u0)
         N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), self.state,
                N.stream(x_init.device))
 

@@ -216,8 +216,10 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
 
 /* ---- the device-resident MPC loop with per-problem trajectory slots ------ */
 /* Caller-owned device buffers of one solve.  Xs and Us hold four trajectories
-   per problem, component-major [4,T,n,B] / [4,T,m,B] for the pendulum and
-   cartpole (coalesced per-lane access) and [4,T,B,n] / [4,T,B,m] for rocket; slot [2,B] (uint8) the indices of each
+   per problem: for the pendulum and cartpole Xs is [4,T,B,n+m] records
+   [x_t; u_t] (a lane moves its record with two wide accesses) and Us is unused
+   (pass Xs); for rocket Xs is [4,T,B,n] and Us [4,T,B,m].  The caller puts
+   u_init (or zeros) into slot 0's u before begin.  slot [2,B] (uint8) the indices of each
    problem's current and best one.  The line search's two candidates roll out
    into the two free slots, so accepting a step size or taking an iterate as
    the new best (mpc_explicit.py:277-283) moves no data.
