@@ -1934,7 +1934,7 @@ inline bool bad_bounds(const dilqr_bounds& b) {
 
 // (n, m) shapes compiled for the generic (LinDx / Riccati / adjoint) kernels.
 // Model kernels use their own fixed shapes.
-#define DILQR_FOR_EACH_SHAPE(X) X(3, 1) X(5, 1) X(4, 3) X(4, 1) X(2, 1) X(4, 2) X(6, 2)
+#define DILQR_FOR_EACH_SHAPE(X) X(3, 1) X(5, 1) X(4, 3) X(4, 1) X(2, 1) X(4, 2) X(6, 2) X(6, 1)
 // shapes served by the 16-lanes-per-problem kernels (dilqr_group.h)
 #define DILQR_FOR_EACH_GROUP_SHAPE(X) X(13, 3)
 #define DILQR_FOR_ALL_SHAPES(X) DILQR_FOR_EACH_SHAPE(X) DILQR_FOR_EACH_GROUP_SHAPE(X)

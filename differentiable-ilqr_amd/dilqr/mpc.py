@@ -1,6 +1,8 @@
 """Classic mpc.pytorch MPC (mpc.py:57-601) on the HIP path.
 
-Takes model dynamics or a LinDx.  The forward loop runs on device; gradients
+Takes model dynamics or a LinDx (and, through dilqr.generic, any dynamics
+Module, AUTO_DIFF / FINITE_DIFF linearisation, non-quadratic costs and the
+slew-rate penalty).  The forward loop runs on device; gradients
 flow through a no-op classic LQR step (lqr_step.py:277-282) whose backward is
 the classic adjoint kernel, exactly like mpc.py:302-335.  With model dynamics
 the reference would also differentiate the autograd linearisation
@@ -16,6 +18,7 @@ from . import _native as N
 from . import ops
 from .definitions import LinDx, QuadCost
 from .lqr_step import LQRStep
+from .mpc_explicit import MPC as ExplicitMPC
 from .mpc_explicit import GradMethods, expand_cost
 
 
@@ -28,9 +31,9 @@ class MPC(Module):
         super().__init__()
         assert (u_lower is None) == (u_upper is None)
         assert max_linesearch_iter > 0
-        for name, val in (("u_zero_I", u_zero_I), ("delta_u", delta_u), ("slew_rate_penalty", slew_rate_penalty)):
-            if val is not None:
-                raise NotImplementedError(f"dilqr: MPC({name}=...) is not on the HIP path")
+        if u_zero_I is not None:
+            raise NotImplementedError("dilqr: MPC(u_zero_I=...) — the mask is internal to the adjoint engine")
+        self.delta_u, self.slew_rate_penalty, self.prev_ctrl = delta_u, slew_rate_penalty, prev_ctrl
         self.n_state, self.n_ctrl, self.T = n_state, n_ctrl, T
         self.u_lower = u_lower if (u_lower is None or isinstance(u_lower, float)) else u_lower.detach()
         self.u_upper = u_upper if (u_upper is None or isinstance(u_upper, float)) else u_upper.detach()
@@ -41,11 +44,22 @@ class MPC(Module):
         self.exit_unconverged, self.detach_unconverged, self.backprop = exit_unconverged, detach_unconverged, backprop
         self.not_improved_lim, self.best_cost_eps = not_improved_lim, best_cost_eps
 
+    # generic dynamics / costs share the explicit MPC's driver
+    forward_generic = ExplicitMPC.forward_generic
+    _detach_unconverged = ExplicitMPC._detach_unconverged
+
+    def fused(self, cost, dx):
+        """The device-resident loop: env_dx model (ANALYTIC) or LinDx, quadratic
+        cost, no slew-rate penalty / delta_u; anything else -> dilqr.generic."""
+        model_ok = isinstance(dx, LinDx) or (getattr(dx, "model_id", None) is not None
+                                             and self.grad_method == GradMethods.ANALYTIC)
+        return isinstance(cost, QuadCost) and model_ok and self.slew_rate_penalty is None and self.delta_u is None
+
     def forward(self, x_init, cost, dx):
-        if not isinstance(cost, QuadCost):
-            raise NotImplementedError("dilqr: non-quadratic costs are not on the HIP path")
         if not x_init.is_cuda:
             raise RuntimeError("dilqr: x_init must be on the GPU (no CPU path)")
+        if not self.fused(cost, dx):
+            return self.forward_generic(x_init, cost, dx, classic=True)
         n_batch = self.n_batch if self.n_batch is not None else (
             cost.C.size(1) if cost.C.ndimension() == 4 else None)
         if n_batch is None:

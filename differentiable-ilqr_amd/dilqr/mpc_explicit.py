@@ -71,19 +71,24 @@ class MPC(Module):
         self.best_cost_eps = best_cost_eps
         self.slew_rate_penalty = slew_rate_penalty
         self.prev_ctrl = prev_ctrl
-        for name, val in (("u_zero_I", u_zero_I), ("delta_u", delta_u), ("slew_rate_penalty", slew_rate_penalty)):
-            if val is not None:
-                raise NotImplementedError(f"dilqr: MPC({name}=...) is not on the HIP path")
-        if grad_method not in (GradMethods.ANALYTIC,):
-            raise NotImplementedError("dilqr: only GradMethods.ANALYTIC linearisation is on the HIP path")
+        if u_zero_I is not None:
+            raise NotImplementedError("dilqr: MPC(u_zero_I=...) — the mask is internal to the adjoint engine")
+        if grad_method == GradMethods.ANALYTIC_CHECK:
+            raise NotImplementedError("dilqr: ANALYTIC_CHECK is disabled in the reference too (mpc_explicit.py:578)")
+
+    def fused(self, cost, dx):
+        """The whole loop in the fused HIP kernels: an env_dx model with its
+        analytic Jacobian, a quadratic cost, no slew-rate penalty / delta_u.
+        Anything else runs the generic loop (dilqr.generic)."""
+        return (isinstance(cost, QuadCost) and getattr(dx, "model_id", None) is not None
+                and self.grad_method == GradMethods.ANALYTIC and self.slew_rate_penalty is None
+                and self.delta_u is None)
 
     def forward(self, x_init, cost, dx):
-        if not isinstance(cost, QuadCost):
-            raise NotImplementedError("dilqr: non-quadratic costs are not on the HIP path")
-        if isinstance(dx, LinDx):
-            raise NotImplementedError("dilqr: mpc_explicit.MPC needs model dynamics (use dilqr.mpc.MPC for LinDx)")
         if not x_init.is_cuda:
             raise RuntimeError("dilqr: x_init must be on the GPU (no CPU path)")
+        if not self.fused(cost, dx):
+            return self.forward_generic(x_init, cost, dx, classic=False)
         n_batch = self.n_batch if self.n_batch is not None else (
             cost.C.size(1) if cost.C.ndimension() == 4 else None)
         if n_batch is None:
@@ -114,6 +119,30 @@ class MPC(Module):
                            true_dynamics=dx, current_x=x, current_u=u, back_eps=self.back_eps,
                            no_op_forward=True)
             x, u = step(x_init, C, c, F, f, th)
+        return self._detach_unconverged(x, u, costs, full_du_norm)
+
+    def forward_generic(self, x_init, cost, dx, classic):
+        """Generic dynamics / costs: dilqr.generic's loop,
+        the HIP Riccati sweep inside, then the closing no-op LQR step."""
+        from . import generic
+        if self.n_batch is not None:
+            n_batch = self.n_batch
+        elif isinstance(cost, QuadCost) and cost.C.ndimension() == 4:
+            n_batch = cost.C.size(1)
+        else:
+            raise ValueError("MPC Error: Could not infer batch size, pass in as n_batch")
+        T, n, m = self.T, self.n_state, self.n_ctrl
+        if isinstance(cost, QuadCost):
+            C, c = expand_cost(cost.C, cost.c, T, n_batch, n + m)
+            cost = QuadCost(C, c)
+        assert x_init.ndimension() == 2 and x_init.size(0) == n_batch
+        x, u, costs, full_du_norm = generic.solve(self, x_init, cost, dx, n_batch)
+        need_grad = torch.is_grad_enabled() and self.backprop
+        if need_grad:
+            x, u = generic.final_step(self, x_init, cost, dx, x, u, classic)
+        return self._detach_unconverged(x, u, costs, full_du_norm)
+
+    def _detach_unconverged(self, x, u, costs, full_du_norm):
         if self.detach_unconverged:
             # mpc_explicit.py:343-356
             if float(full_du_norm.max()) > self.eps:

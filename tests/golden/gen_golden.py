@@ -552,11 +552,101 @@ def case_il():
     save("il", **out)
 
 
+# --------------------------------------------------------------------------
+# J. generic dynamics / costs: NNDynamics with
+#    AUTO_DIFF / FINITE_DIFF / ANALYTIC (grad_input) linearisation through the
+#    classic mpc.MPC (+ its backward into the network), an env_dx model with
+#    AUTO_DIFF through mpc_explicit, a non-quadratic cost (approximate_cost),
+#    and the slew-rate augmentation.  fp64 and fp32.
+# --------------------------------------------------------------------------
+class NQCost(torch.nn.Module):
+    """A smooth non-quadratic stage cost: 1/2|tau|^2 + 0.1 sum tau^4 + w . tau."""
+
+    def __init__(self, w):
+        super().__init__()
+        self.w = w
+
+    def forward(self, tau):
+        return 0.5 * (tau ** 2).sum(-1) + 0.1 * (tau ** 4).sum(-1) + (tau * self.w).sum(-1)
+
+
+def case_generic():
+    print("J. generic dynamics / costs")
+    for dt in (torch.float64, torch.float32):
+        generic_one(dt)
+
+
+def generic_one(dt):
+    import dynamics as ref_dyn
+    out = {}
+    with default_dtype(dt), contextlib.redirect_stdout(io.StringIO()):
+        T, B = 10, 8
+        rng = np.random.RandomState(21)
+        # ---- NNDynamics (n=5, m=1, one hidden layer of 32 sigmoids), classic MPC
+        torch.manual_seed(3)
+        nn_dx = ref_dyn.NNDynamics(5, 1, hidden_sizes=[32], activation="sigmoid")
+        for i, fc in enumerate(nn_dx.fcs):
+            out[f"nn_W{i}"], out[f"nn_b{i}"] = np_(fc.weight), np_(fc.bias)
+        x0 = 0.3 * rng.normal(size=(B, 5))
+        L = rng.normal(size=(T, B, 6, 6)) * 0.3
+        C = L @ np.swapaxes(L, -1, -2) + np.eye(6)
+        c = 0.1 * rng.normal(size=(T, B, 6))
+        wx, wu = rng.normal(size=(T, B, 5)), rng.normal(size=(T, B, 1))
+        out.update(nn_x0=x0, nn_C=C, nn_c=c, nn_wx=wx, nn_wu=wu)
+        for tag, gm in (("auto", R.mpc.GradMethods.AUTO_DIFF), ("fd", R.mpc.GradMethods.FINITE_DIFF),
+                        ("analytic", R.mpc.GradMethods.ANALYTIC)):
+            for p_ in nn_dx.parameters():
+                p_.grad = None
+            X0 = torch.tensor(x0, dtype=dt, requires_grad=True)
+            Ct, ct = torch.tensor(C, dtype=dt, requires_grad=True), torch.tensor(c, dtype=dt, requires_grad=True)
+            m = R.mpc.MPC(5, 1, T, lqr_iter=4, grad_method=gm, u_lower=-1.0, u_upper=1.0, n_batch=B,
+                          exit_unconverged=False, detach_unconverged=False, linesearch_decay=0.2,
+                          max_linesearch_iter=10)
+            x, u, costs = m(X0, R.mpc.QuadCost(Ct, ct), nn_dx)
+            ((x * torch.tensor(wx, dtype=dt)).sum() + (u * torch.tensor(wu, dtype=dt)).sum()).backward()
+            out.update({f"nn_{tag}_x": np_(x), f"nn_{tag}_u": np_(u), f"nn_{tag}_costs": np_(costs),
+                        f"nn_{tag}_dx0": np_(X0.grad), f"nn_{tag}_dC": np_(Ct.grad), f"nn_{tag}_dc": np_(ct.grad)})
+            for i, fc in enumerate(nn_dx.fcs):
+                out[f"nn_{tag}_dW{i}"] = np_(fc.weight.grad)
+                out[f"nn_{tag}_db{i}"] = np_(fc.bias.grad)
+        # ---- cartpole through mpc_explicit with AUTO_DIFF (forward)
+        dx = model("cartpole")
+        x0c = xinit_for("cartpole", B, rng)
+        Q, P = true_cost(dx, T, B, dt)
+        m = R.mpc_explicit.MPC(5, 1, T, lqr_iter=5, grad_method=R.mpc_explicit.GradMethods.AUTO_DIFF,
+                               exit_unconverged=False, detach_unconverged=False, linesearch_decay=0.5,
+                               max_linesearch_iter=2, eps=0.0, not_improved_lim=10 ** 9)
+        x, u, costs = m(torch.tensor(x0c, dtype=dt), R.mpc_explicit.QuadCost(Q, P), dx)
+        out.update(cart_auto_x0=x0c, cart_auto_x=np_(x), cart_auto_u=np_(u), cart_auto_costs=np_(costs))
+        # ---- cartpole with a slew-rate penalty: mpc_explicit ANALYTIC and mpc AUTO_DIFF (forward)
+        for tag, mod, gm in (("slew_explicit", R.mpc_explicit, R.mpc_explicit.GradMethods.ANALYTIC),
+                             ("slew_classic", R.mpc, R.mpc.GradMethods.AUTO_DIFF)):
+            m = mod.MPC(5, 1, T, lqr_iter=5, grad_method=gm, slew_rate_penalty=0.1, exit_unconverged=False,
+                        detach_unconverged=False, linesearch_decay=0.5, max_linesearch_iter=2, eps=0.0,
+                        not_improved_lim=10 ** 9)
+            x, u, costs = m(torch.tensor(x0c, dtype=dt), mod.QuadCost(Q, P), dx)
+            out.update({f"{tag}_x": np_(x), f"{tag}_u": np_(u), f"{tag}_costs": np_(costs)})
+        # ---- pendulum with a non-quadratic cost: mpc AUTO_DIFF and mpc_explicit ANALYTIC (forward)
+        dxp = model("pendulum")
+        x0p = xinit_for("pendulum", B, rng)
+        wq = 0.3 * rng.normal(size=4)
+        out.update(nq_x0=x0p, nq_w=wq)
+        for tag, mod, gm in (("nq_classic", R.mpc, R.mpc.GradMethods.AUTO_DIFF),
+                             ("nq_explicit", R.mpc_explicit, R.mpc_explicit.GradMethods.ANALYTIC)):
+            m = mod.MPC(3, 1, T, lqr_iter=5, grad_method=gm, n_batch=B, exit_unconverged=False,
+                        detach_unconverged=False, linesearch_decay=0.2, max_linesearch_iter=5, eps=0.0,
+                        not_improved_lim=10 ** 9, u_lower=-2.0, u_upper=2.0)
+            x, u, costs = m(torch.tensor(x0p, dtype=dt), NQCost(torch.tensor(wq, dtype=dt)), dxp)
+            out.update({f"{tag}_x": np_(x), f"{tag}_u": np_(u), f"{tag}_costs": np_(costs)})
+    save(f"generic_{tname(dt)}", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["models", "riccati", "pnqp", "lqrstep", "mpc", "adjoint", "implicit",
-                             "datasets", "il"]
+                             "datasets", "il", "generic"]
     table = {"models": case_models, "riccati": case_riccati, "pnqp": case_pnqp,
              "lqrstep": case_lqrstep, "mpc": case_mpc, "adjoint": case_classic_adjoint,
-             "implicit": case_implicit, "datasets": case_datasets, "il": case_il}
+             "implicit": case_implicit, "datasets": case_datasets, "il": case_il,
+             "generic": case_generic}
     for w in which:
         table[w]()
