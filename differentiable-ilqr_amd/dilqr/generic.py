@@ -220,8 +220,18 @@ def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u
     B = x.shape[1]
     lo = u_lower if (u_lower is None or isinstance(u_lower, float)) else u_lower.detach().contiguous()
     hi = u_upper if (u_upper is None or isinstance(u_upper, float)) else u_upper.detach().contiguous()
+    rlo, rhi = lo, hi
+    if delta_u is not None and lo is not None:
+        # lqr_step_explicit.py:132-135: the sweep's box is also clipped to
+        # +-delta_u around u_t; as absolute bounds for the kernel (which forms
+        # bound - u_t) that is max(lower, u_t - delta_u) / min(upper, u_t + delta_u)
+        ud = u.detach()
+        lo_t = lo if isinstance(lo, torch.Tensor) else torch.full_like(ud, lo)
+        hi_t = hi if isinstance(hi, torch.Tensor) else torch.full_like(ud, hi)
+        rlo = torch.where(lo_t - ud < -delta_u, ud - delta_u, lo_t).contiguous()
+        rhi = torch.where(hi_t - ud > delta_u, ud + delta_u, hi_t).contiguous()
     K, k, _ = ops.lqr_backward(C.detach().contiguous(), c.detach().contiguous(), F.detach().contiguous(), n, m,
-                               x=x.detach().contiguous(), u=u.detach().contiguous(), u_lower=lo, u_upper=hi)
+                               x=x.detach().contiguous(), u=u.detach().contiguous(), u_lower=rlo, u_upper=rhi)
     old_cost = traj_cost(T, x, u, true_cost)
     alphas = torch.ones(B, device=x.device)
     cur_cost, full_du_norm = None, None

@@ -626,6 +626,13 @@ def generic_one(dt):
                         not_improved_lim=10 ** 9)
             x, u, costs = m(torch.tensor(x0c, dtype=dt), mod.QuadCost(Q, P), dx)
             out.update({f"{tag}_x": np_(x), f"{tag}_u": np_(u), f"{tag}_costs": np_(costs)})
+        # ---- cartpole with the delta_u trust region (lqr_step_explicit.py:205-213)
+        m = R.mpc_explicit.MPC(5, 1, T, lqr_iter=5, grad_method=R.mpc_explicit.GradMethods.ANALYTIC,
+                               u_lower=-10.0, u_upper=10.0, delta_u=1.0, exit_unconverged=False,
+                               detach_unconverged=False, linesearch_decay=0.5, max_linesearch_iter=2, eps=0.0,
+                               not_improved_lim=10 ** 9)
+        x, u, costs = m(torch.tensor(x0c, dtype=dt), R.mpc_explicit.QuadCost(Q, P), dx)
+        out.update(delta_u_x=np_(x), delta_u_u=np_(u), delta_u_costs=np_(costs))
         # ---- pendulum with a non-quadratic cost: mpc AUTO_DIFF and mpc_explicit ANALYTIC (forward)
         dxp = model("pendulum")
         x0p = xinit_for("pendulum", B, rng)

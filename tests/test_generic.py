@@ -143,3 +143,19 @@ def test_non_quadratic_cost(golden, tag):
         x, u, costs = m(gpu(g["nq_x0"]), NQCost(gpu(g["nq_w"])), PendulumDx())
     assert relerr(cpu(costs), g[f"{tag}_costs"]) < 1e-3
     assert relerr(cpu(u), g[f"{tag}_u"]) < 1e-3
+
+
+def test_delta_u_trust_region(golden):
+    """delta_u: each step's control stays within +-delta_u of the current one,
+    inside the box (lqr_step_explicit.py:205-213)."""
+    import dilqr
+    g = golden("generic_f32")
+    T, B = g["delta_u_x"].shape[:2]
+    dx, C, c = cart_cost(T, B)
+    m = dilqr.MPC(5, 1, T, lqr_iter=5, u_lower=-10.0, u_upper=10.0, delta_u=1.0, exit_unconverged=False,
+                  detach_unconverged=False, linesearch_decay=0.5, max_linesearch_iter=2, eps=0.0,
+                  not_improved_lim=10 ** 9)
+    with torch.no_grad():
+        x, u, costs = m(gpu(g["cart_auto_x0"]), dilqr.QuadCost(C, c), dx)
+    assert relerr(cpu(costs), g["delta_u_costs"]) < 1e-3
+    assert relerr(cpu(u), g["delta_u_u"]) < 1e-3

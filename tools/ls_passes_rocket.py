@@ -1,0 +1,39 @@
+"""Config 3 (rocket): per iteration, the share of problems and of waves (4
+problems) that need more than one paired line-search pass (alpha < decay)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "differentiable-ilqr_amd"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from dilqr import _native as N  # noqa: E402
+from dilqr import ops  # noqa: E402
+from dilqr.env_dx.rocket import RocketDx  # noqa: E402
+
+dev = torch.device("cuda", 0)
+T, B, n, m = 30, 32768, 13, 3
+rng = np.random.RandomState(0)
+r = rng.uniform([0, -4, -2.5], [10, 4, 2.5], (B, 3))
+v = rng.normal(0, 0.1, (B, 3))
+q4 = np.array([1., 0, 0, 0]) + 0.05 * rng.normal(size=(B, 4))
+q4 /= np.linalg.norm(q4, axis=1, keepdims=True)
+w = rng.normal(0, 0.02, (B, 3))
+x0 = torch.tensor(np.concatenate([r, v, q4, w], 1), dtype=torch.float32, device=dev)
+dx = RocketDx()
+q, p = dx.get_true_obj()
+C = torch.diag(q).repeat(T, B, 1, 1).to(dev).contiguous()
+c = p.repeat(T, B, 1).to(dev).contiguous()
+theta = ops.theta_of(dx, x0)
+sv = ops.MPCSolve(T, B, n, m, dev)
+nb, _ = N.make_bounds(None, None)
+sv.begin(N.MODEL_ROCKET, theta, x0)
+for i in range(10):
+    sv.iterate(N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, i, 1e-4, 0.0, 10 ** 9)
+    a = sv.alpha.view(-1, 4)
+    more = (a < 0.2 - 1e-7).float()
+    hist = {f"{x:g}": int((sv.alpha == x).sum()) for x in (1.0, 0.2, 0.04, 0.008, 0.0016)}
+    print(f"iter {i}: problems >1 pair pass {float(more.mean()):.3f}, waves {float(more.max(1).values.mean()):.3f}"
+          f"  alpha hist {hist}", flush=True)
