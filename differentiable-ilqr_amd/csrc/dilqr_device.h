@@ -51,6 +51,84 @@ DEV void vsincos(f2 x, f2& s, f2& c) {
 DEV float vclamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 DEV f2 vclamp(f2 x, float lo, float hi) { return f2{fminf(fmaxf(x.x, lo), hi), fminf(fmaxf(x.y, lo), hi)}; }
 
+// Hardware reciprocal / reciprocal square root (v_rcp_f32 / v_rsq_f32, 1 ulp)
+// and explicit fused multiply-add, per component.
+DEV float vrcp(float x) { return __builtin_amdgcn_rcpf(x); }
+DEV f2 vrcp(f2 x) { return f2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; }
+DEV float vrsq(float x) { return __builtin_amdgcn_rsqf(x); }
+DEV f2 vrsq(f2 x) { return f2{__builtin_amdgcn_rsqf(x.x), __builtin_amdgcn_rsqf(x.y)}; }
+DEV float vfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+DEV f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// sin and cos of a moderate angle: Cody-Waite reduction by pi/2 (three-part
+// constant, fma), minimax polynomials on [-pi/4, pi/4] (Cephes sinf/cosf
+// coefficients), quadrant fix-up.  |d| > 8192, inf and NaN take ocml's sincosf.
+// The polynomial part is written once for float and f2, so the two
+// line-search candidates evaluate it as packed fp32 ops.
+DEV void sincos_quadrant(int q, float s1, float c1, float& s, float& c) {
+  const float ss = (q & 1) ? c1 : s1, cc = (q & 1) ? s1 : c1;
+  s = (q & 2) ? -ss : ss;
+  c = ((q + 1) & 2) ? -cc : cc;
+}
+template <class S>
+DEV void sincos_poly(S r, S& s1, S& c1) {
+  const S z = r * r;
+  s1 = vfma(vfma(vfma(S(-1.9515295891e-4f), z, S(8.3321608736e-3f)), z, S(-1.6666654611e-1f)) * z, r, r);
+  c1 = vfma(vfma(vfma(S(2.443315711809948e-5f), z, S(-1.388731625493765e-3f)), z, S(4.166664568298827e-2f)),
+            z * z, S(-0.5f) * z) + S(1.0f);
+}
+DEV void sincos_fast(float d, float& s, float& c) {
+  if (!(fabsf(d) <= 8192.f)) { sincosf(d, &s, &c); return; }
+  const float k = __builtin_rintf(d * 0.636619772f);
+  float r = vfma(-k, 1.5703125f, d);
+  r = vfma(-k, 4.837512969970703125e-4f, r);
+  r = vfma(-k, 7.54978995489188216e-8f, r);
+  float s1, c1;
+  sincos_poly(r, s1, c1);
+  sincos_quadrant((int)k, s1, c1, s, c);
+}
+DEV void sincos_fast(f2 d, f2& s, f2& c) {
+  if (!(fabsf(d.x) <= 8192.f) || !(fabsf(d.y) <= 8192.f)) {
+    float s0, c0, s1, c1;
+    sincos_fast(d.x, s0, c0);
+    sincos_fast(d.y, s1, c1);
+    s = f2{s0, s1}; c = f2{c0, c1};
+    return;
+  }
+  const f2 k = f2{__builtin_rintf(d.x * 0.636619772f), __builtin_rintf(d.y * 0.636619772f)};
+  f2 r = vfma(-k, f2(1.5703125f), d);
+  r = vfma(-k, f2(4.837512969970703125e-4f), r);
+  r = vfma(-k, f2(7.54978995489188216e-8f), r);
+  f2 s1, c1;
+  sincos_poly(r, s1, c1);
+  float sa, ca, sb, cb;
+  sincos_quadrant((int)k.x, s1.x, c1.x, sa, ca);
+  sincos_quadrant((int)k.y, s1.y, c1.y, sb, cb);
+  s = f2{sa, sb}; c = f2{ca, cb};
+}
+
+// cos and sin of atan2(s, c) + delta without the atan2 (the angle update of the
+// pendulum and cartpole dynamics, pendulum.py:88-93, cartpole.py:87-95): with
+// r = |(c, s)|, cos(atan2(s, c)) = c / r and sin(atan2(s, c)) = s / r, so the
+// angle-sum formulas need sin and cos of the small increment delta only.
+// atan2(0, 0) = 0: a zero (c, s) acts as (1, 0).
+template <class S>
+DEV void angle_step(S c, S s, S delta, S& co, S& so) {
+  S sd, cd;
+  sincos_fast(delta, sd, cd);
+  const S r2 = c * c + s * s;
+  const S ir = vrsq(r2);
+  S cn = c * ir, sn = s * ir;
+  if constexpr (sizeof(S) == sizeof(float)) {
+    if (r2 == 0.f) { cn = 1.f; sn = 0.f; }
+  } else {
+    if (r2.x == 0.f) { cn.x = 1.f; sn.x = 0.f; }
+    if (r2.y == 0.f) { cn.y = 1.f; sn.y = 0.f; }
+  }
+  co = cn * cd - sn * sd;
+  so = sn * cd + cn * sd;
+}
+
 // ------------------------------------------------------------------ loads/stores
 // Vectorised load/store of one lane's contiguous record of K floats.  Record
 // offsets are multiples of K floats and the base is 16-byte aligned (checked on
@@ -525,7 +603,21 @@ struct RiccatiState {
     }
 
     // V = Qxx + Qxu K + K^T Qux + (K^T Quu) K ; v = qx + Qxu k + K^T qu + (K^T Quu) k
-    // (lqr_step_explicit.py:157-160)
+    // (lqr_step_explicit.py:157-160).  Unconstrained m = 1, where K = -Qux/Quu and
+    // k = -qu/Quu: the last two terms cancel (K^T Qux = -(K^T Quu) K, K^T qu =
+    // -(K^T Quu) k), leaving the Schur complement V = Qxx + Qxu K, v = qx + Qxu k.
+    if constexpr (MODE == GAIN_UNC && M == 1) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+#pragma unroll
+        for (int j = SYM ? i : 0; j < N; ++j) {
+          V[i][j] = Q[i][N] * K[0][j] + Q[i][j];
+          if (SYM && j != i) V[j][i] = V[i][j];
+        }
+        v[i] = Q[i][N] * k[0] + q[i];
+      }
+      return;
+    }
     float KtQuu[N][M];
 #pragma unroll
     for (int i = 0; i < N; ++i)

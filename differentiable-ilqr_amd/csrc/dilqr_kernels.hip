@@ -923,6 +923,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     SweepIn<n, m, TL, BM> cur, n1, n2;
     cur.load(cs, x, u, bd, T - 1, B, b);
     if constexpr (kPF >= 2) n1.load(cs, x, u, bd, T > 1 ? T - 2 : 0, B, b);
+#pragma unroll 2
     for (int t = T - 1; t >= 0; --t) {
       if constexpr (kPF >= 2) n2.load(cs, x, u, bd, t > 1 ? t - 2 : 0, B, b);   // prefetch step t-2
       else n1.load(cs, x, u, bd, t > 0 ? t - 1 : 0, B, b);                       // prefetch step t-1

@@ -1,7 +1,10 @@
 // dilqr_models.h — device dynamics of the reference's env_dx models.
 //
-// forward(): op-for-op restatement of the reference forward (contraction off,
-// so every product/sum rounds like the reference's eager fp32 ops).
+// forward(): the reference forward's arithmetic, restated for the GPU: rocket
+// op for op (contraction off); pendulum and cartpole with the angle update
+// through angle_step (dilqr_device.h: the angle-sum identity instead of
+// atan2 -> add -> sin/cos) and the divisions as reciprocal products — the same
+// function to a few ulp (tests: dynamics vs the reference at 2e-5).
 // jacobian(): d x_{t+1} / d [x_t;u_t] at the UNCLAMPED u, as get_linear_dyn
 // writes it, derived by hand with common subexpressions.
 #pragma once
@@ -16,7 +19,12 @@ struct Pendulum {
   static constexpr float DT = 0.05f;
   static constexpr float ULIM = 2.0f;      // forward() clamps u to [-ULIM, ULIM]
   float g, m, l;
-  DEV void load(const float* __restrict__ th) { g = th[0]; m = th[1]; l = th[2]; }
+  float kg, ku;                            // 3g/(2l), 3/(m l^2)
+  DEV void load(const float* __restrict__ th) {
+    g = th[0]; m = th[1]; l = th[2];
+    kg = 3.0f * g / (2.0f * l);
+    ku = 3.0f / (m * (l * l));
+  }
 
   static constexpr bool kJacFromNext = false;   // its Jacobian angle uses the unclamped u
   DEV void jacobian_next(const float (&x)[N], const float (&u)[M], const float (&)[N], float (&D)[N][N + M]) const {
@@ -27,32 +35,26 @@ struct Pendulum {
     static constexpr bool nz(int i, int j) { return !(i == 2 && j == 0); }
   };
 
-  // pendulum.py:60-95; S = float, or f2 for two trajectories at once
+  // pendulum.py:60-95; S = float, or f2 for two trajectories at once.  The
+  // angle update th' = atan2(sin, cos) + dt * dth' goes through angle_step (no
+  // atan2; sin and cos of the increment only)
   template <class S>
   DEV void forward(const S (&x)[N], const S (&u)[M], S (&o)[N]) const {
-#pragma clang fp contract(off)
     S uu = vclamp(u[0], -2.0f, 2.0f);
     S c = x[0], s = x[1], dth = x[2];
-    S th = vatan2(s, c);
-    S a = (-3.0f * g) / (2.0f * l) * (-s);
-    S b = (3.0f * uu) / (m * (l * l));
-    S newdth = dth + DT * (a + b);
-    S newth = th + newdth * DT;
-    vsincos(newth, o[1], o[0]);
+    S newdth = dth + DT * (kg * s + ku * uu);
+    angle_step(c, s, newdth * DT, o[0], o[1]);
     o[2] = newdth;
   }
 
   // pendulum.py:444-475
   DEV void jacobian(const float (&x)[N], const float (&u)[M], float (&D)[N][N + M]) const {
     float c = x[0], s = x[1], dth = x[2], uu = u[0];
-    float r2 = c * c + s * s;
-    float kg = 3.0f * g / (2.0f * l);
-    float ku = 3.0f / (l * l * m);
-    float newth = DT * (DT * (kg * s + ku * uu) + dth) + atan2f(s, c);
     float sn, cs;
-    vsincos(newth, sn, cs);
-    float dc = -s / r2;                 // d newth / d cos
-    float ds = c / r2 + DT * DT * kg;   // d newth / d sin
+    angle_step(c, s, DT * (DT * (kg * s + ku * uu) + dth), cs, sn);
+    float ir2 = vrcp(c * c + s * s);
+    float dc = -s * ir2;                // d newth / d cos
+    float ds = c * ir2 + DT * DT * kg;  // d newth / d sin
     float dw = DT;                      // d newth / d dth
     float du = DT * DT * ku;            // d newth / d u
     D[0][0] = -sn * dc; D[0][1] = -sn * ds; D[0][2] = -sn * dw; D[0][3] = -sn * du;
@@ -69,7 +71,14 @@ struct Cartpole {
   static constexpr float DT = 0.05f;
   static constexpr float ULIM = 100.0f;
   float g, mc, mp, l;
-  DEV void load(const float* __restrict__ th) { g = th[0]; mc = th[1]; mp = th[2]; l = th[3]; }
+  float iM, pml, mpM, pmlM;                // 1/(mc+mp), mp l, mp/(mc+mp), mp l/(mc+mp)
+  DEV void load(const float* __restrict__ th) {
+    g = th[0]; mc = th[1]; mp = th[2]; l = th[3];
+    iM = 1.0f / (mp + mc);
+    pml = mp * l;
+    mpM = mp * iM;
+    pmlM = pml * iM;
+  }
 
   // structural nonzeros of jacobian() (cartpole.py:802-838): rows x, dx, cos, sin, dth
   struct FSparsity {
@@ -78,44 +87,33 @@ struct Cartpole {
     }
   };
 
-  // cartpole.py:64-97; S = float, or f2 for two trajectories at once
+  // cartpole.py:64-97; S = float, or f2 for two trajectories at once.  The
+  // divisions by the mass are products with 1/(mc+mp), the one by the
+  // pole-inertia term a hardware reciprocal, and th' = atan2(sin, cos) + dt*dth
+  // goes through angle_step (no atan2; sin and cos of dt*dth only).
   template <class S>
   DEV void forward(const S (&s_)[N], const S (&u)[M], S (&o)[N]) const {
-#pragma clang fp contract(off)
-    float total_mass = mp + mc;
-    float pml = mp * l;
     S uu = vclamp(u[0], -100.0f, 100.0f);
     S x = s_[0], dx = s_[1], c = s_[2], s = s_[3], dth = s_[4];
-    S th = vatan2(s, c);
-    S cart_in = (uu + (pml * (dth * dth)) * s) / total_mass;
-    S th_acc = (g * s - c * cart_in) / (l * (4.0f / 3.0f - (mp * (c * c)) / total_mass));
-    S xacc = cart_in - ((pml * th_acc) * c) / total_mass;
+    S cart_in = (uu + (pml * (dth * dth)) * s) * iM;
+    S th_acc = (g * s - c * cart_in) * vrcp(l * (4.0f / 3.0f - mpM * (c * c)));
+    S xacc = cart_in - (pmlM * th_acc) * c;
     o[0] = x + DT * dx;
     o[1] = dx + DT * xacc;
-    S th2 = th + DT * dth;
-    vsincos(th2, o[3], o[2]);
+    angle_step(c, s, DT * dth, o[2], o[3]);
     o[4] = dth + DT * th_acc;
-  }
-
-  // the angle forward() integrates to, rounded as forward() and the reference's
-  // dt * dth + atan2(sin, cos) (cartpole.py:825-834) round it: no contraction
-  DEV static float next_angle(float c, float s, float w) {
-#pragma clang fp contract(off)
-    return atan2f(s, c) + DT * w;
   }
 
   // cartpole.py:790-839 (closed form of the same derivative)
   DEV void jacobian(const float (&s_)[N], const float (&u)[M], float (&D)[N][N + M]) const {
-    const float th2 = next_angle(s_[2], s_[3], s_[4]);
     float sn, cs;
-    vsincos(th2, sn, cs);
+    angle_step(s_[2], s_[3], DT * s_[4], cs, sn);
     jacobian_sc(s_, u, cs, sn, D);
   }
 
   // The Jacobian's cos/sin of the integrated angle are exactly components 2 and
-  // 3 of forward(x, u) (same angle, same rounding, independent of u), so along a
-  // rollout the fused sweep takes them from x_{t+1} instead of recomputing
-  // atan2, sin and cos.
+  // 3 of forward(x, u) (the same angle_step call, independent of u), so along a
+  // rollout the fused sweep takes them from x_{t+1} instead of recomputing them.
   static constexpr bool kJacFromNext = true;
   DEV void jacobian_next(const float (&s_)[N], const float (&u)[M], const float (&xn)[N],
                          float (&D)[N][N + M]) const {
@@ -124,11 +122,9 @@ struct Cartpole {
 
   DEV void jacobian_sc(const float (&s_)[N], const float (&u)[M], float cs, float sn, float (&D)[N][N + M]) const {
     float c = s_[2], s = s_[3], w = s_[4], uu = u[0];
-    float Mt = mc + mp, iM = 1.0f / Mt;
-    float pml = mp * l;
     float A = uu + pml * w * w * s;                 // cart_in * M
     float den = l * (4.0f / 3.0f - mp * c * c * iM);
-    float iden = 1.0f / den;
+    float iden = vrcp(den);
     float num = g * s - c * A * iM;
     float tha = num * iden;                         // th_acc
     // partials of A, den, num wrt (c, s, w, u)
@@ -137,12 +133,12 @@ struct Cartpole {
     float num_c = -A * iM, num_s = g - c * A_s * iM, num_w = -c * A_w * iM, num_u = -c * iM;
     float tha_c = (num_c - tha * den_c) * iden;
     float tha_s = num_s * iden, tha_w = num_w * iden, tha_u = num_u * iden;
-    float k = pml * iM;
+    float k = pmlM;
     float xa_c = -k * (tha_c * c + tha);
     float xa_s = A_s * iM - k * tha_s * c;
     float xa_w = A_w * iM - k * tha_w * c;
     float xa_u = iM - k * tha_u * c;
-    float ir2 = 1.0f / (c * c + s * s);
+    float ir2 = vrcp(c * c + s * s);
     D[0][0] = 1.f; D[0][1] = DT;  D[0][2] = 0.f;            D[0][3] = 0.f;            D[0][4] = 0.f;            D[0][5] = 0.f;
     D[1][0] = 0.f; D[1][1] = 1.f; D[1][2] = DT * xa_c;      D[1][3] = DT * xa_s;      D[1][4] = DT * xa_w;      D[1][5] = DT * xa_u;
     D[2][0] = 0.f; D[2][1] = 0.f; D[2][2] = s * sn * ir2;   D[2][3] = -c * sn * ir2;  D[2][4] = -DT * sn;       D[2][5] = 0.f;

@@ -239,7 +239,7 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
    clamped to the box) — begin and the line search write only such
    trajectories.  The fused sweep relies on it: models whose Jacobian needs the
    integrated angle's cos/sin (cartpole) take them from x_{t+1} instead of
-   recomputing atan2, cos and sin.  Do not write into Xs/Us from outside. */
+   recomputing them from x_t.  Do not write into Xs/Us from outside. */
 typedef struct dilqr_mpc_state {
   float* Xs; float* Us; unsigned char* slot; float* best_cost; float* best_du;
   int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;
