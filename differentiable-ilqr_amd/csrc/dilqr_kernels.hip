@@ -13,6 +13,10 @@ namespace dilqr {
 constexpr int kBlock = 64;   // one wave per workgroup: 64 problems, 4 workgroups per CU
                              // at B=65536, freely distributed over the 8 XCDs.
 constexpr size_t kLdsPerCU = 160 * 1024;   // CDNA4 LDS per CU
+#ifndef DILQR_NO_LDS_GAINS
+#define DILQR_NO_LDS_GAINS 0
+#endif
+constexpr bool kNoLdsGains = DILQR_NO_LDS_GAINS;   // test builds: gain records in HBM always
 
 static inline int grid_for(long long n) { return (int)((n + kBlock - 1) / kBlock); }
 
@@ -764,6 +768,10 @@ struct FwdIn {
 #define DILQR_PF 1
 #endif
 constexpr int kPF = DILQR_PF;
+#ifndef DILQR_PF_LS
+#define DILQR_PF_LS 2
+#endif
+constexpr int kPFL = DILQR_PF_LS;                   // the line search's prefetch distance
 
 // ---------------- forward: the line search (lqr_step_explicit.py:166-263).
 // Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
@@ -811,9 +819,9 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
       float x0r[n];
       ld_xu<TL>(x0r, cur.u, x, u, 0, B, b);
     }
-    if constexpr (kPF >= 2) n1.load(ws, u, cs, x, bd, T, cl(1), cl(2), B, b);
+    if constexpr (kPFL >= 2) n1.load(ws, u, cs, x, bd, T, cl(1), cl(2), B, b);
     for (int t = 0; t < T; ++t) {
-      if constexpr (kPF >= 2) n2.load(ws, u, cs, x, bd, T, cl(t + 2), cl(t + 3), B, b);   // prefetch step t+2
+      if constexpr (kPFL >= 2) n2.load(ws, u, cs, x, bd, T, cl(t + 2), cl(t + 3), B, b);   // prefetch step t+2
       else n1.load(ws, u, cs, x, bd, T, cl(t + 1), cl(t + 2), B, b);                      // prefetch step t+1
       f2 nu[m];
 #pragma unroll
@@ -876,7 +884,7 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
         for (int a = 0; a < m; ++a) n1.u[a] = cur.unext[a];     // u_{t+1}
       }
       cur = n1;
-      if constexpr (kPF >= 2) n1 = n2;
+      if constexpr (kPFL >= 2) n1 = n2;
     }
     const float cA = cp.x, cB = cp.y;
     if (!(cA > old_cost) || p == max_ls - 1) { cost = cA; alpha = aA; win = 0; break; }
@@ -1231,33 +1239,61 @@ template <bool STAGE>
 __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iteration, MpcState S) {
   // the block's rows are one contiguous span of TM*blockDim floats: stage it
   // through LDS with coalesced loads, then each thread sums its row (stride TM
-  // words; TM odd -> conflict-free, TM even -> at most 2-way)
+  // words; TM odd -> conflict-free, TM even -> at most 2-way).  Every global
+  // load (the control flag, improved[r], the span) is issued before the first
+  // one is waited on: the kernel is one HBM latency, not three in a row.
   extern __shared__ __attribute__((aligned(16))) float sdu[];
   __shared__ unsigned red_max[4];
   __shared__ int red_any[4];
-  if (S.ctrl[iteration & 1].stopped) return;          // iteration `iteration` did not run
-  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int stopped = S.ctrl[iteration & 1].stopped;   // iteration `iteration` did not run: acted on below
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int imp = r < B ? S.improved[r] : 0;
   if constexpr (STAGE) {
     const size_t base = (size_t)blockIdx.x * blockDim.x * TM;
     const size_t total = (size_t)B * TM;
     const int span = blockDim.x * TM;
-    // up to 32 independent loads in flight per thread before the first LDS
-    // store (a load->store loop would serialise one HBM latency per element)
-    constexpr int U = 32;
-    for (int i0 = threadIdx.x; i0 < span; i0 += blockDim.x * U) {
-      float v[U];
+    const int have = (int)((total - base) < (size_t)span ? total - base : (size_t)span);
+    if ((span & 3) == 0 && (have & 3) == 0) {          // base is then 16-byte aligned too
+      // up to 8 float4 loads in flight per thread (span <= 64 KiB = 4096 float4)
+      constexpr int U = 8;
+      const float4* src = reinterpret_cast<const float4*>(S.du_sq + base);
+      float4* dst = reinterpret_cast<float4*>(sdu);
+      const int n4 = span >> 2, h4 = have >> 2;
+      for (int i0 = threadIdx.x; i0 < n4; i0 += blockDim.x * U) {
+        float4 v[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const int i = i0 + j * blockDim.x;
-        v[j] = (i < span && base + i < total) ? S.du_sq[base + i] : 0.f;
+        for (int j = 0; j < U; ++j) {
+          const int i = i0 + j * blockDim.x;
+          v[j] = i < h4 ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          const int i = i0 + j * blockDim.x;
+          if (i < n4) dst[i] = v[j];
+        }
       }
+    } else {
+      // up to 32 independent loads in flight per thread before the first LDS
+      // store (a load->store loop would serialise one HBM latency per element)
+      constexpr int U = 32;
+      for (int i0 = threadIdx.x; i0 < span; i0 += blockDim.x * U) {
+        float v[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const int i = i0 + j * blockDim.x;
-        if (i < span) sdu[i] = v[j];
+        for (int j = 0; j < U; ++j) {
+          const int i = i0 + j * blockDim.x;
+          v[j] = i < have ? S.du_sq[base + i] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          const int i = i0 + j * blockDim.x;
+          if (i < span) sdu[i] = v[j];
+        }
       }
     }
+    if (stopped) return;                               // uniform over the grid
     __syncthreads();
+  } else {
+    if (stopped) return;
   }
   unsigned mx = 0u;
   int any = 0;
@@ -1268,7 +1304,6 @@ __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iterat
     float fdn = sqrtf(s);
     S.full_du_norm[r] = fdn;
     mx = __float_as_uint(fdn);              // fdn >= 0: float order == uint order
-    int imp = S.improved[r];
     if (imp) S.best_du[r] = fdn;
     any = imp == 2;
   }
@@ -2343,7 +2378,7 @@ int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float*
 #define LAUNCH_MPC(BM_)                                                                                      \
   do {                                                                                                       \
     const size_t lds = (size_t)T * kBlock * (MD::N * MD::M + MD::M) * sizeof(float);                        \
-    if (lds * 4 <= kLdsPerCU)                                                                                \
+    if (lds * 4 <= kLdsPerCU && !kNoLdsGains)                                                                \
       k_mpc_iterate<MD, BM_, true><<<grid_for(B), kBlock, lds, S(stream)>>>(                                 \
           T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, \
           lim, G, st);                                                                                       \
