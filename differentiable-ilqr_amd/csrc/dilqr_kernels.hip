@@ -1364,11 +1364,13 @@ template <class Model>
 constexpr int slot_layout() { return Model::N + Model::M <= 8 ? TRAJ_REC : TRAJ_AOS; }
 constexpr int slot_layout_nm(int n, int m) { return n + m <= 8 ? TRAJ_REC : TRAJ_AOS; }
 
-// rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl.  The
-// caller has placed u_init (or zeros) in slot 0's u.
+// rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl.
+// u_init: the caller's [T,B,m] controls, or null for zeros (the MPC default):
+// read once, written into the slot with the states in the same pass.
 template <class Model>
 __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float* __restrict__ theta,
-                                                      const float* __restrict__ x_init, MpcState S) {
+                                                      const float* __restrict__ x_init,
+                                                      const float* __restrict__ u_init, MpcState S) {
   constexpr int n = Model::N, m = Model::M;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b == 0) {
@@ -1385,8 +1387,13 @@ __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float*
   float xt[n];
   ld(xt, x_init + (size_t)b * n);
   for (int t = 0; t < T; ++t) {
-    float ut[m], xo[n], xn[n];
-    ld_xu<TL>(xo, ut, S.Xs, S.Us, t, B, b);
+    float ut[m], xn[n];
+    if (u_init) {
+      ld(ut, u_init + ((size_t)t * B + b) * m);
+    } else {
+#pragma unroll
+      for (int a = 0; a < m; ++a) ut[a] = 0.f;
+    }
     st_xu<TL>(S.Xs, S.Us, xt, ut, t, B, b);
     if (t < T - 1) {
       md.forward(xt, ut, xn);
@@ -2004,7 +2011,7 @@ inline int launch_norm_rows(int TM, int B, int iteration, const MpcState& st, hi
 
 extern "C" {
 
-int dilqr_version(void) { return 1; }
+int dilqr_version(void) { return 2; }
 
 int dilqr_model_num_ctrl(int model) {
   switch (model) {
@@ -2345,10 +2352,12 @@ int dilqr_mpc_packed_cost_floats(int n, int m) {
   return d < 1 ? -1 : d * (d + 1) / 2 + d;
 }
 
-int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init, dilqr_mpc_state st,
-                        void* stream) {
+int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init, const float* u_init,
+                        dilqr_mpc_state st, void* stream) {
   if (T < 1 || B < 0 || !theta || !x_init || !al16(x_init) || bad_state(st)) return DILQR_E_ARG;
-  MODEL_SWITCH(model, (k_mpc_begin<MD><<<grid_for(B > 0 ? B : 1), kBlock, 0, S(stream)>>>(T, B, theta, x_init, st)));
+  if (u_init && ((uintptr_t)u_init & 3u)) return DILQR_E_ARG;
+  MODEL_SWITCH(model, (k_mpc_begin<MD><<<grid_for(B > 0 ? B : 1), kBlock, 0, S(stream)>>>(T, B, theta, x_init, u_init,
+                                                                                          st)));
   return launched();
 }
 

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must be imported first: libdilqr.so then binds to t
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DILQR_LIB", os.path.join(_HERE, "libdilqr.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MODEL_LINDX, MODEL_PENDULUM, MODEL_CARTPOLE, MODEL_ROCKET = 0, 1, 2, 3
 BOUNDS_NONE, BOUNDS_SCALAR, BOUNDS_TENSOR = 0, 1, 2
@@ -58,7 +58,7 @@ SIGNATURES = {
                                _vp, _vp, _vp, _vp], _i),
     "dilqr_implicit_ws_floats": ([_i], _i),
     "dilqr_mpc_packed_cost_floats": ([_i, _i], _i),
-    "dilqr_mpc_begin_f32": ([_i, _i, _i, _vp, _vp, MpcState, _vp], _i),
+    "dilqr_mpc_begin_f32": ([_i, _i, _i, _vp, _vp, _vp, MpcState, _vp], _i),
     "dilqr_mpc_iterate_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
     "dilqr_mpc_step_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
     "dilqr_mpc_stop_rule_f32": ([_i, _i, _i, _i, MpcState, _vp], _i),

@@ -189,16 +189,18 @@ class MPCSolve:
 
     def begin(self, model_id, theta, x_init, u_init=None):
         """x = get_traj(u_init or 0) into slot 0; reset slots and the control block."""
-        u_slot0 = self.Xs[0, :, :, self.n:] if self.rec else self.Us[0]
-        if u_init is None:
-            u_slot0.zero_()
-        else:
+        u0 = None
+        if u_init is not None:
             u0 = u_init.to(device=self.Xs.device, dtype=torch.float32)
             if u0.ndimension() == 2:
                 u0 = u0.unsqueeze(1).expand(self.T, self.B, self.m)
-            u_slot0.copy_(u0)
-        N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), self.state,
-               N.stream(x_init.device))
+            u0 = u0.contiguous()
+            if tuple(u0.shape) != (self.T, self.B, self.m):
+                raise ValueError(f"u_init: expected [T, B, m] = {(self.T, self.B, self.m)} or [T, m], got "
+                                 f"{tuple(u_init.shape)}")
+        N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init),
+               None if u0 is None else N.ptr(u0), self.state, N.stream(x_init.device))
+        self._u0 = u0                       # alive until the launch has read it
 
     def iterate(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, iteration, best_cost_eps, eps,
                 not_improved_lim):

@@ -247,11 +247,12 @@ typedef struct dilqr_mpc_state {
   unsigned char* cost_sym;
 } dilqr_mpc_state;
 
-/* Start a solve: x = get_traj(u) from the controls the caller placed in Us
-   slot 0 (zeros or u_init), slots/ctrl reset (mpc_explicit.py:228-249). */
+/* Start a solve: slot 0 = (get_traj(u), u) with u = u_init ([T,B,m], the
+   caller's controls) or zeros when u_init is NULL; slots/ctrl reset
+   (mpc_explicit.py:228-249, util.py:104-127). */
 int dilqr_mpc_packed_cost_floats(int n, int m);
 int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init,
-                        dilqr_mpc_state st, void* stream);
+                        const float* u_init, dilqr_mpc_state st, void* stream);
 
 /* One MPC iteration (mpc_explicit.py:246-299), iteration = 0, 1, ... of the
    solve.  Two launches: (1) the stop rule for iteration-1 (mpc_explicit.py:264,
