@@ -1063,11 +1063,7 @@ __global__ void __launch_bounds__(kBlock) k_ilqr_iterate(int T, int B, const flo
 using MpcState = dilqr_mpc_state;
 constexpr int kSlots = 4;
 
-DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim, bool fast);
-DEV bool mpc_rows_pending(const MpcState& S, int k);
-template <bool LG>
-DEV void mpc_pending_rows(const MpcState& S, int T, int m, int B, int k, int b, int imp, float* lds);
-DEV void mpc_any_partial(const MpcState& S, int B, int k, bool improved2);
+DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim);
 
 // the two lowest slot indices not in {cur, best}
 DEV void free_slots(int cur, int best, int& sa, int& sb) {
@@ -1093,17 +1089,11 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
                                                         int iteration, float best_cost_eps, float eps,
                                                         int not_improved_lim, int G, MpcState S) {
   constexpr int n = Model::N, m = Model::M;
-  const bool fast = !(eps > 0.f);                          // stop rule without the row max (see mpc_decide)
-  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim, fast)) return;
+  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   const int first = iteration == 0;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  // rows of iteration-1 when no stop-rule kernel ran (done at the end, below;
-  // improved[] of iteration-1 is read now, before this launch overwrites it)
-  const bool pend = mpc_rows_pending(S, iteration);
-  const int imp_prev = pend ? S.improved[b] : 0;
   Model md; md.load(theta);
-  float* const du_sq = S.du_sq + (size_t)(iteration & 1) * T * m * B;   // this iteration's plane
   const size_t TBd = (size_t)T * B * (n + m);               // one slot: [T,B,d] records
   const int cur = S.slot[b], best = S.slot[B + b];
   int sa, sb;
@@ -1125,7 +1115,7 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
     if constexpr (packed_diag_ok<n + m>()) {
       CostDiagConst<n + m> cc;
       cc.init(S.Cpk, T, B, b);
-      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr, du_sq, cost,
+      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
                                                 alpha);
     } else {
       __builtin_unreachable();
@@ -1135,21 +1125,21 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
       win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr, nullptr,
                                           xcur, nullptr, bd, decay, max_ls, gr,
                                           xsa, nullptr, xsb, nullptr,
-                                          du_sq, cost, alpha);
+                                          S.du_sq, cost, alpha);
     else
       __builtin_unreachable();
   } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
     win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T}, nullptr,
                                     nullptr, xcur, nullptr, bd, decay, max_ls, gr,
-                                    xsa, nullptr, xsb, nullptr, du_sq,
+                                    xsa, nullptr, xsb, nullptr, S.du_sq,
                                     cost, alpha);
   else if (pk & kCostSym)
     win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
-                                    xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr, du_sq, cost, alpha);
+                                    xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost, alpha);
   else
     win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
                                     first && S.Cpk ? S.cost_sym : nullptr, xcur, nullptr, bd,
-                                    decay, max_ls, gr, xsa, nullptr, xsb, nullptr, du_sq, cost, alpha);
+                                    decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost, alpha);
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
   S.alpha[b] = alpha;
@@ -1160,8 +1150,6 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   }
   S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
   S.slot[b] = (unsigned char)nw;
-  if (fast) mpc_any_partial(S, B, iteration, better);
-  if (pend) mpc_pending_rows<LG>(S, T, m, B, iteration, b, imp_prev, lds_gains);
 }
 
 // the same two kernels for the 16-lanes-per-problem models (dilqr_group.h)
@@ -1201,7 +1189,7 @@ __global__ void __launch_bounds__(64) k_mpc_iterate_group(int T, int B, const fl
                                                           MpcState S) {
   constexpr int n = Model::N, m = Model::M;
   __shared__ GroupLds<n, m> Ls[kGPW];
-  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim, false)) return;
+  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   const int first = iteration == 0;
   const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
   const int b0 = blockIdx.x * kGPW + gp;
@@ -1216,8 +1204,7 @@ __global__ void __launch_bounds__(64) k_mpc_iterate_group(int T, int B, const fl
   int win;
   group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, S.Xs + cur * TBn, S.Us + cur * TBm,
                                   bd, decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
-                                  S.Us + sb * TBm, S.du_sq + (size_t)(iteration & 1) * T * m * B, cost,
-                                  alpha, win);
+                                  S.Us + sb * TBm, S.du_sq, cost, alpha, win);
   const int nw = win ? sb : sa;
   if (valid && r == 0) {
     S.cost[b] = cost;
@@ -1261,7 +1248,6 @@ __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iterat
   const int stopped = S.ctrl[iteration & 1].stopped;   // iteration `iteration` did not run: acted on below
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   const int imp = r < B ? S.improved[r] : 0;
-  const float* __restrict__ du_sq = S.du_sq + (size_t)(iteration & 1) * TM * B;   // the iteration's plane
   if constexpr (STAGE) {
     const size_t base = (size_t)blockIdx.x * blockDim.x * TM;
     const size_t total = (size_t)B * TM;
@@ -1270,7 +1256,7 @@ __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iterat
     if ((span & 3) == 0 && (have & 3) == 0) {          // base is then 16-byte aligned too
       // up to 8 float4 loads in flight per thread (span <= 64 KiB = 4096 float4)
       constexpr int U = 8;
-      const float4* src = reinterpret_cast<const float4*>(du_sq + base);
+      const float4* src = reinterpret_cast<const float4*>(S.du_sq + base);
       float4* dst = reinterpret_cast<float4*>(sdu);
       const int n4 = span >> 2, h4 = have >> 2;
       for (int i0 = threadIdx.x; i0 < n4; i0 += blockDim.x * U) {
@@ -1295,7 +1281,7 @@ __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iterat
 #pragma unroll
         for (int j = 0; j < U; ++j) {
           const int i = i0 + j * blockDim.x;
-          v[j] = i < have ? du_sq[base + i] : 0.f;
+          v[j] = i < have ? S.du_sq[base + i] : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
@@ -1313,7 +1299,7 @@ __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iterat
   int any = 0;
   if (r < B) {
     float s = 0.f;
-    const float* p = STAGE ? sdu + (size_t)threadIdx.x * TM : du_sq + (size_t)r * TM;
+    const float* p = STAGE ? sdu + (size_t)threadIdx.x * TM : S.du_sq + (size_t)r * TM;
     for (int i = 0; i < TM; ++i) s += p[i];
     float fdn = sqrtf(s);
     S.full_du_norm[r] = fdn;
@@ -1338,119 +1324,37 @@ __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iterat
   }
 }
 
-// Prologue of iteration k (one 64-lane wave per workgroup): the stop rule for
-// iteration k-1, published as S_k in ctrl[k&1].  Returns true when the solve has
-// stopped (the wave exits).
-// fast (eps <= 0, the thread-per-problem kernels): `max full_du_norm < eps` can
-// never hold (norms are >= 0, NaN compares false), so the rule needs no row max
-// and no stop-rule kernel runs: the step kernel writes the per-workgroup "any
-// improved" partials itself (mpc_any_partial), and the quirk rows + best_du of
-// iteration k are computed by the NEXT launch (mpc_pending_rows; the final
-// iteration's by dilqr_mpc_gather_best_f32).  ctrl.rows_pending = k+1 marks
-// them; du_sq is double-buffered by iteration parity so they are still there.
-// The value of eps must not change within a solve.
-DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim, bool fast) {
-  dilqr_mpc_ctrl out = {};                             // S_0: begin zeroed ctrl[0..1]
-  if (k > 0) {
-    const dilqr_mpc_ctrl in = S.ctrl[(k - 1) & 1];      // S_{k-1}
-    out = in;
-    if (!in.stopped) {
-      const bool have_max = in.rows_pending != k;        // a stop-rule kernel ran after iteration k-1
-      const int gm = sync_gmax(B), par = (k - 1) & 1;
-      const unsigned* pm = S.done_counter + 16 + (2 * par) * gm;
-      const unsigned* pa = S.done_counter + 16 + (2 * par + 1) * gm;
-      const int lane = threadIdx.x & 63;
-      unsigned mx = 0u;
-      int any = 0;
-      for (int i = lane; i < G; i += 64) {
-        if (have_max) {
-          unsigned v = pm[i];
-          mx = v > mx ? v : mx;
-        }
-        any |= (int)pa[i];
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        unsigned o = __shfl_xor(mx, off, 64);
-        mx = o > mx ? o : mx;
-        any |= __shfl_xor(any, off, 64);
-      }
-      out.iter = in.iter + 1;
-      out.n_not_improved = any ? 0 : in.n_not_improved + 1;     // mpc_explicit.py:264, 279
-      out.max_du_bits = mx;
-      if ((have_max && __uint_as_float(mx) < eps) || out.n_not_improved > not_improved_lim)   // 297-299
-        out.stopped = 1;
+// Prologue of iteration k >= 1 (one 64-lane wave per workgroup): the stop rule
+// for iteration k-1.  Returns true when the solve has stopped (the wave exits).
+DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim) {
+  if (k == 0) return false;                            // S_0: begin zeroed ctrl[0..1]
+  const dilqr_mpc_ctrl in = S.ctrl[(k - 1) & 1];        // S_{k-1}
+  dilqr_mpc_ctrl out = in;
+  if (!in.stopped) {
+    const int gm = sync_gmax(B), par = (k - 1) & 1;
+    const unsigned* pm = S.done_counter + 16 + (2 * par) * gm;
+    const unsigned* pa = S.done_counter + 16 + (2 * par + 1) * gm;
+    const int lane = threadIdx.x & 63;
+    unsigned mx = 0u;
+    int any = 0;
+    for (int i = lane; i < G; i += 64) {
+      unsigned v = pm[i];
+      mx = v > mx ? v : mx;
+      any |= (int)pa[i];
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      unsigned o = __shfl_xor(mx, off, 64);
+      mx = o > mx ? o : mx;
+      any |= __shfl_xor(any, off, 64);
+    }
+    out.iter = in.iter + 1;
+    out.n_not_improved = any ? 0 : in.n_not_improved + 1;     // mpc_explicit.py:264, 279
+    out.max_du_bits = mx;
+    if (__uint_as_float(mx) < eps || out.n_not_improved > not_improved_lim) out.stopped = 1;   // 297-299
   }
-  out.seq = k + 1;
-  if (!out.stopped) out.rows_pending = fast ? k + 1 : 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) S.ctrl[k & 1] = out;
   return out.stopped != 0;
-}
-
-// The quirk row r = b of the iteration whose rows are pending (ctrl.rows_pending
-// = it + 1): full_du_norm[b] and, when problem b improved in that iteration,
-// best_du[b] — the values k_mpc_norm_rows writes (same summation order).
-DEV void mpc_row_store(const MpcState& S, int b, float s, int imp) {
-  const float fdn = sqrtf(s);
-  S.full_du_norm[b] = fdn;
-  if (imp) S.best_du[b] = fdn;
-}
-DEV void mpc_rows_of(const MpcState& S, int T, int m, int B, int it, int b, int imp) {
-  const int TM = T * m;
-  const float* p = S.du_sq + (size_t)(it & 1) * TM * B + (size_t)b * TM;
-  float s = 0.f;
-  for (int i = 0; i < TM; ++i) s += p[i];
-  mpc_row_store(S, b, s, imp);
-}
-
-DEV bool mpc_rows_pending(const MpcState& S, int k) {
-  return k > 0 && S.ctrl[(k - 1) & 1].rows_pending == k;
-}
-
-// At the end of launch k: the rows of k-1 for this workgroup's problems.  With
-// the gain records in LDS (free again once the line search is done) and a full
-// workgroup, its 64 rows — one contiguous span of 64*T*m floats — are staged
-// with coalesced float4 loads and summed from LDS (stride T*m words); else each
-// lane reads its row directly.
-template <bool LG>
-DEV void mpc_pending_rows(const MpcState& S, int T, int m, int B, int k, int b, int imp, float* lds) {
-  const int TM = T * m;
-  const int blk0 = b - (int)(threadIdx.x & 63);
-  if (LG && blk0 + 64 <= B) {
-    const float4* src = reinterpret_cast<const float4*>(S.du_sq + (size_t)((k - 1) & 1) * TM * B + (size_t)blk0 * TM);
-    float4* dst = reinterpret_cast<float4*>(lds);
-    const int n4 = 16 * TM;                             // 64*TM floats
-    const int l = threadIdx.x & 63;
-    for (int i0 = l; i0 < n4; i0 += 256) {              // four float4 loads in flight per lane
-      const int i1 = i0 + 64, i2 = i0 + 128, i3 = i0 + 192;
-      const float4 a0 = src[i0];
-      const float4 a1 = src[i1 < n4 ? i1 : i0];
-      const float4 a2 = src[i2 < n4 ? i2 : i0];
-      const float4 a3 = src[i3 < n4 ? i3 : i0];
-      dst[i0] = a0;
-      if (i1 < n4) dst[i1] = a1;
-      if (i2 < n4) dst[i2] = a2;
-      if (i3 < n4) dst[i3] = a3;
-    }
-    __syncthreads();
-    const float* p = lds + (size_t)l * TM;
-    float s = 0.f;
-    for (int i = 0; i < TM; ++i) s += p[i];
-    mpc_row_store(S, b, s, imp);
-  } else {
-    mpc_rows_of(S, T, m, B, k - 1, b, imp);
-  }
-}
-
-// "any problem improved" (mpc_explicit.py:279) of this workgroup in iteration k,
-// into the partials plane the next prologue reduces (index: workgroup)
-DEV void mpc_any_partial(const MpcState& S, int B, int k, bool improved2) {
-  const unsigned long long bal = __ballot(improved2);
-  if ((threadIdx.x & 63) == 0) {
-    const int gm = sync_gmax(B), par = k & 1;
-    S.done_counter[16 + (2 * par + 1) * gm + blockIdx.x] = bal != 0ull ? 1u : 0u;
-  }
 }
 
 // slot layout: [T,B,d] records for the thread-per-problem models (TRAJ_REC;
@@ -1504,11 +1408,6 @@ __global__ void __launch_bounds__(kBlock) k_mpc_gather(int T, int B, MpcState S,
                                                        float* __restrict__ u_out) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  {                                                    // rows of the last iteration, if still pending
-    const dilqr_mpc_ctrl c0 = S.ctrl[0], c1 = S.ctrl[1];
-    const int pend = c1.seq > c0.seq ? c1.rows_pending : c0.rows_pending;
-    if (pend > 0) mpc_rows_of(S, T, m, B, pend - 1, b, S.improved[b]);
-  }
   int best = S.slot[B + b];
   constexpr int TL = slot_layout_nm(n, m);
   const float* X = S.Xs + (size_t)best * T * B * (TL == TRAJ_REC ? n + m : n);
@@ -2098,9 +1997,6 @@ inline NormGeom norm_geom(int TM, int B) {
   return {threads, (B + threads - 1) / threads, stage};
 }
 
-// the stop rule without a row max (mpc_decide): eps <= 0, thread-per-problem models
-inline bool mpc_fast(int model, float eps) { return model != DILQR_MODEL_ROCKET && !(eps > 0.f); }
-
 inline int launch_norm_rows(int TM, int B, int iteration, const MpcState& st, hipStream_t stream) {
   const NormGeom g = norm_geom(TM, B);
   if (g.stage)
@@ -2474,9 +2370,7 @@ int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float*
   if (B == 0) return 0;
   const int m = dilqr_model_num_ctrl(model);
   if (m < 1) return DILQR_E_SHAPE;
-  // partials of the previous iteration: per stop-rule block, or per step
-  // workgroup in fast mode (mpc_decide)
-  const int G = mpc_fast(model, eps) ? grid_for(B) : norm_geom(T * m, B).blocks;
+  const int G = norm_geom(T * m, B).blocks;            // partials of the previous iteration's rows
   const int lim = not_improved_lim;
   Bounds bd = mkb(bounds);
   bool box = bounds.mode != DILQR_BOUNDS_NONE;
@@ -2527,7 +2421,6 @@ int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const flo
   int e = dilqr_mpc_step_f32(model, T, B, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter,
                              iteration, best_cost_eps, eps, not_improved_lim, st, stream);
   if (e) return e;
-  if (mpc_fast(model, eps)) return 0;                  // rows deferred to the next launch (mpc_decide)
   return dilqr_mpc_stop_rule_f32(T, m, B, iteration, st, stream);
 }
 

@@ -172,7 +172,7 @@ class MPCSolve:
         self.improved = torch.zeros(B, dtype=torch.int32, device=dev)
         self.cost = torch.empty(B, device=dev)
         self.alpha = torch.empty(B, device=dev)
-        self.du_sq = torch.empty(2, T, m, B, device=dev)       # double-buffered by iteration parity
+        self.du_sq = torch.empty(T, m, B, device=dev)
         self.full_du_norm = torch.empty(B, device=dev)
         self.ws = torch.empty(T * B * ilqr_ws_floats(n, m), device=dev)
         self.ctrl = torch.zeros(2 * N.CTRL_INTS, dtype=torch.int32, device=dev)   # ping-pong control state

@@ -143,10 +143,7 @@ typedef struct dilqr_mpc_ctrl {
   int n_not_improved;    /* mpc_explicit.py:264, 279                     */
   int any_improved;      /* scratch for the current iteration            */
   unsigned max_du_bits;  /* float bits of max(full_du_norm) this iter    */
-  int seq;               /* 1 + the iteration index that published it    */
-  int rows_pending;      /* 1 + the iteration whose quirk rows / best_du
-                            are not computed yet (eps <= 0 solves), or 0 */
-  int pad;
+  int pad[3];
 } dilqr_mpc_ctrl;
 
 /* Projected-Newton box QP, pnqp.py:5-82, per problem (the reference at batch
@@ -221,13 +218,11 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
 /* Caller-owned device buffers of one solve.  Xs and Us hold four trajectories
    per problem: for the pendulum and cartpole Xs is [4,T,B,n+m] records
    [x_t; u_t] (a lane moves its record with two wide accesses) and Us is unused
-   (pass Xs); for rocket Xs is [4,T,B,n] and Us [4,T,B,m].  slot [2,B] (uint8) the indices of each
+   (pass Xs); for rocket Xs is [4,T,B,n] and Us [4,T,B,m].  The caller puts
+   u_init (or zeros) into slot 0's u before begin.  slot [2,B] (uint8) the indices of each
    problem's current and best one.  The line search's two candidates roll out
    into the two free slots, so accepting a step size or taking an iterate as
    the new best (mpc_explicit.py:277-283) moves no data.
-   du_sq: 2*T*m*B floats ([2,T,m,B]: the first line-search pass's (u-u')^2,
-   double-buffered by iteration parity).  best_du / full_du_norm [B]: the quirk
-   rows (lqr_step_explicit.py:245-247); complete after dilqr_mpc_gather_best_f32.
    ws: T*B*ceil4(m*n+m+1) floats.  done_counter: the stop rule's sync area of
    16 + 4*ceil(B/64) uints.  ctrl: two dilqr_mpc_ctrl (ping-pong, zeroed by begin).
    Cpk (nullable) + cost_sym [B] (uint8): the solve's packed copy of a
@@ -267,11 +262,7 @@ int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float
    full_du_norm rows, best_du and per-workgroup partials of this iteration for
    the next prologue.  Once stopped, iterations are no-ops.  The control state
    after the decisions for iterations 0..k-1 is in ctrl[k&1] (ctrl points to two
-   dilqr_mpc_ctrl).  = dilqr_mpc_step_f32 + dilqr_mpc_stop_rule_f32, except for
-   eps <= 0 with the pendulum / cartpole models: `max full_du_norm < eps` cannot
-   hold, so only (1) runs; it also computes the previous iteration's rows and
-   writes the "any improved" partials, and gather_best finishes the last
-   iteration's rows.  eps must be the same for every iteration of a solve. */
+   dilqr_mpc_ctrl).  = dilqr_mpc_step_f32 + dilqr_mpc_stop_rule_f32. */
 int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const float* x_init,
                           const float* C, const float* c, dilqr_bounds bounds,
                           float linesearch_decay, int max_linesearch_iter, int iteration,

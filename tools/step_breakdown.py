@@ -1,9 +1,7 @@
 """Where one headline solve's time goes (config 2: cartpole T=25, 65536 problems,
 10 fixed iterations): HIP events around begin (u = 0 fill + rollout), iteration
 0 (reads the caller's C, builds the packed copy), iterations 1..9 and the
-stop-rule kernel after each (launched explicitly), then whole solves through
-MPCSolve.iterate (eps = 0: no stop-rule kernel).  Prints one JSON line of
-per-launch averages."""
+stop-rule kernel after each.  Prints one JSON line of per-launch averages."""
 import json
 import os
 import sys
@@ -52,15 +50,6 @@ for solve in range(SOLVES):
         N.call("dilqr_mpc_stop_rule_f32", T, m, B, i, sv.state, s)
         row.append(ev())
     marks.append(row)
-# the same solves as the library's MPC iterate runs them (eps = 0: no stop-rule
-# kernel; the next launch computes the rows)
-whole = []
-for solve in range(SOLVES):
-    e0 = ev()
-    sv.begin(N.MODEL_CARTPOLE, theta, x0)
-    for i in range(ITERS):
-        sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, i, 1e-4, 0.0, 10 ** 9)
-    whole.append((e0, ev()))
 torch.cuda.synchronize()
 res = {"begin": [], "iter0": [], "iterk": [], "stop_rule": [], "solve": []}
 for row in marks[1:]:                       # the first solve warms up
@@ -72,7 +61,5 @@ for row in marks[1:]:                       # the first solve warms up
         res["stop_rule"].append(b_.elapsed_time(c_))
 out = {k: float(np.mean(v)) for k, v in res.items()}
 out["per_iteration_of_solve"] = out["solve"] / ITERS
-out["solve_iterate"] = float(np.mean([a.elapsed_time(b_) for a, b_ in whole[1:]]))
-out["per_iteration_iterate"] = out["solve_iterate"] / ITERS
 out["B"] = B
 print(json.dumps(out))
