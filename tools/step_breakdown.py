@@ -1,7 +1,9 @@
 """Where one headline solve's time goes (config 2: cartpole T=25, 65536 problems,
 10 fixed iterations): HIP events around begin (u = 0 fill + rollout), iteration
 0 (reads the caller's C, builds the packed copy), iterations 1..9 and the
-stop-rule kernel after each.  Prints one JSON line of per-launch averages."""
+stop-rule kernel after each, then whole solves through MPCSolve.iterate with no
+events in between (`solve_iterate`: the number to compare variants by — the
+events themselves add a few us per launch).  Prints one JSON line."""
 import json
 import os
 import sys
@@ -50,6 +52,14 @@ for solve in range(SOLVES):
         N.call("dilqr_mpc_stop_rule_f32", T, m, B, i, sv.state, s)
         row.append(ev())
     marks.append(row)
+# the same solves as the bench runs them: no events between the launches
+whole = []
+for solve in range(SOLVES):
+    e0 = ev()
+    sv.begin(N.MODEL_CARTPOLE, theta, x0)
+    for i in range(ITERS):
+        sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, i, 1e-4, 0.0, 10 ** 9)
+    whole.append((e0, ev()))
 torch.cuda.synchronize()
 res = {"begin": [], "iter0": [], "iterk": [], "stop_rule": [], "solve": []}
 for row in marks[1:]:                       # the first solve warms up
@@ -61,5 +71,7 @@ for row in marks[1:]:                       # the first solve warms up
         res["stop_rule"].append(b_.elapsed_time(c_))
 out = {k: float(np.mean(v)) for k, v in res.items()}
 out["per_iteration_of_solve"] = out["solve"] / ITERS
+out["solve_iterate"] = float(np.mean([a.elapsed_time(b_) for a, b_ in whole[1:]]))
+out["per_iteration_iterate"] = out["solve_iterate"] / ITERS
 out["B"] = B
 print(json.dumps(out))
