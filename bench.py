@@ -123,13 +123,17 @@ def _timed_solves(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, lqr_iter
 
 
 def _event_ms(stream, fn, reps):
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    """Average time of fn(r), r = 0..reps-1, launched back to back between ONE
+    pair of HIP events on `stream` (an event pair around every launch adds
+    several us of its own to a 40-us kernel; rocprof's kernel durations agree
+    with this figure, profiles/)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
     for r in range(reps):
-        ev[r][0].record(stream)
         fn(r)
-        ev[r][1].record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
-    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return e0.elapsed_time(e1) / reps
 
 
 def riccati_workload(n, m, T, B, dev, seed=0):
@@ -188,15 +192,9 @@ def dense_cost_roofline(dev, x0, theta, B, reps=10):
     stream = torch.cuda.current_stream(dev)
     sv.begin(N.MODEL_CARTPOLE, theta, x0)
     sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for r in range(reps):
-        ev[r][0].record(stream)
-        N.call("dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T, B, N.ptr(theta), N.ptr(x0), N.ptr(C), N.ptr(c), nb, 0.5,
-               2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s)
-        ev[r][1].record(stream)
-        N.call("dilqr_mpc_stop_rule_f32", T, N_CTRL, B, r + 1, sv.state, s)
-    torch.cuda.synchronize(dev)
-    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    ms = _event_ms(stream, lambda r: N.call("dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T, B, N.ptr(theta), N.ptr(x0),
+                                            N.ptr(C), N.ptr(c), nb, 0.5, 2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s),
+                   reps)
     cf = iter_cost_floats(sv.cost_sym.cpu().numpy())
     nbytes = float(iter_bytes_per_problem(cf).sum())
     gbs = nbytes / (ms * 1e-3) / 1e9
@@ -401,22 +399,17 @@ def main():
         elapsed = float(tt.item())
     assert args.kernels_only or bool(torch.isfinite(sv.best_cost).all()), "non-finite costs"
 
-    # ---- roofline of the dominant kernel: the fused MPC iteration kernel
-    # (k_mpc_iterate), timed with HIP events on ITS stream (the current stream,
-    # where ops launch it); the stop-rule kernel runs outside the events
+    # ---- roofline of the dominant kernel: the steady-state fused MPC iteration
+    # kernel (k_mpc_iterate<..., FIRST=false>), iterations 1..reps of a solve
+    # launched back to back between one pair of HIP events on ITS stream (the
+    # current stream, where ops launch it).  No stop-rule launches in between:
+    # with eps = 0 and not_improved_lim = inf the rule cannot fire.
     reps = 10
-    # (iterations 1..reps of a solve: iteration 0 also builds the packed cost copy)
     sv.begin(N.MODEL_CARTPOLE, theta, x0)
     sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for r in range(reps):
-        ev[r][0].record(stream)
-        N.call("dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C), N.ptr(c),
-               bounds, 0.5, 2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s)
-        ev[r][1].record(stream)
-        N.call("dilqr_mpc_stop_rule_f32", T_HORIZON, N_CTRL, B, r + 1, sv.state, s)
-    torch.cuda.synchronize(dev)
-    iter_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    iter_ms = _event_ms(stream, lambda r: N.call(
+        "dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C), N.ptr(c), bounds,
+        0.5, 2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s), reps)
     cost_floats = iter_cost_floats(sv.cost_sym.cpu().numpy())
     iter_bytes = float(iter_bytes_per_problem(cost_floats).sum())
     cost_path = ("time-invariant diagonal cost held in registers (2d floats per problem)"
@@ -429,14 +422,9 @@ def main():
     k = torch.empty(T_HORIZON, B, N_CTRL, device=dev)
     cb = torch.randn(T_HORIZON, B, D, device=dev)
     nb = N.Bounds(N.BOUNDS_NONE, 0.0, 0.0, None, None)
-    sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for r in range(reps):
-        sev[r][0].record(stream)
-        N.call("dilqr_lqr_backward_f32", N_STATE, N_CTRL, T_HORIZON, B, N.ptr(C), N.ptr(cb), None, None, N.ptr(F),
-               nb, None, 0, N.ptr(K), N.ptr(k), None, s)
-        sev[r][1].record(stream)
-    torch.cuda.synchronize(dev)
-    sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in sev]))
+    sweep_ms = _event_ms(stream, lambda r: N.call(
+        "dilqr_lqr_backward_f32", N_STATE, N_CTRL, T_HORIZON, B, N.ptr(C), N.ptr(cb), None, None, N.ptr(F), nb, None,
+        0, N.ptr(K), N.ptr(k), None, s), reps)
     sweep_bytes = SWEEP_BYTES_PER_PROBLEM * B
 
     # PMC figures of the same kernel at this shape (tools/profile_pmc.sh over
@@ -479,7 +467,7 @@ def main():
                        "batch_per_gpu": B, "global_batch": B_total, "T": T_HORIZON,
                        "parallelism": f"batch-sharded x{world} (no collective)",
                        "batch_iters_per_s": world * args.steps / elapsed},
-            "roofline": {"kernel": "k_mpc_iterate<Cartpole,UNC,LDS gains> (fused linearise+Riccati+line search; "
+            "roofline": {"kernel": "k_mpc_iterate<Cartpole,UNC,LDS gains,steady> (fused linearise+Riccati+line search; "
                                    + cost_path + ")",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -1082,7 +1082,10 @@ DEV void free_slots(int cur, int best, int& sa, int& sb) {
 // LG: the gain records live in this workgroup's LDS (dynamic, T*64*GREC floats;
 // dilqr_mpc_step_f32 picks it when 4 workgroups per CU still fit the 160 KB),
 // instead of a workspace round trip through HBM/MALL every iteration.
-template <class Model, int BM, bool LG>
+// FIRST: iteration 0 of the solve (reads the caller's C, c and builds the
+// packed copy) — its own instantiation, so the steady-state kernel carries no
+// copy-building code and profiles separately.
+template <class Model, int BM, bool LG, bool FIRST>
 __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const float* __restrict__ theta,
                                                         const float* __restrict__ x_init, const float* __restrict__ C,
                                                         const float* __restrict__ c, Bounds bd, float decay, int max_ls,
@@ -1090,7 +1093,7 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
                                                         int not_improved_lim, int G, MpcState S) {
   constexpr int n = Model::N, m = Model::M;
   if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
-  const int first = iteration == 0;
+  constexpr bool first = FIRST;                             // == (iteration == 0), chosen by the host
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   Model md; md.load(theta);
@@ -1110,36 +1113,42 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   // symmetric, reading only diag(C_t) and c_t when they are all diagonal too
   // (per-lane flags; a wave normally takes one side of the branch)
   const CostFull<n + m> full{C, c};
-  const unsigned char pk = (!first && S.Cpk) ? S.cost_sym[b] : 0;
-  if ((pk & (kCostDiag | kCostTinv)) == (kCostDiag | kCostTinv)) {
-    if constexpr (packed_diag_ok<n + m>()) {
-      CostDiagConst<n + m> cc;
-      cc.init(S.Cpk, T, B, b);
-      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
-                                                alpha);
-    } else {
-      __builtin_unreachable();
-    }
-  } else if (pk & kCostDiag) {           // set by iteration 0 only when packed_diag_ok
-    if constexpr (packed_diag_ok<n + m>())
-      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr, nullptr,
-                                          xcur, nullptr, bd, decay, max_ls, gr,
-                                          xsa, nullptr, xsb, nullptr,
-                                          S.du_sq, cost, alpha);
+  if constexpr (FIRST) {
+    win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, S.Cpk, S.Cpk ? S.cost_sym : nullptr,
+                                                  xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
+                                                  S.du_sq, cost, alpha);
+  } else {
+    const unsigned char pk = S.Cpk ? S.cost_sym[b] : 0;
+    if ((pk & (kCostDiag | kCostTinv)) == (kCostDiag | kCostTinv)) {
+      if constexpr (packed_diag_ok<n + m>()) {
+        CostDiagConst<n + m> cc;
+        cc.init(S.Cpk, T, B, b);
+        win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd,
+                                                      decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
+                                                      alpha);
+      } else {
+        __builtin_unreachable();
+      }
+    } else if (pk & kCostDiag) {           // set by iteration 0 only when packed_diag_ok
+      if constexpr (packed_diag_ok<n + m>())
+        win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr,
+                                                      nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb,
+                                                      nullptr, S.du_sq, cost, alpha);
+      else
+        __builtin_unreachable();
+    } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
+      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T},
+                                                    nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr,
+                                                    xsb, nullptr, S.du_sq, cost, alpha);
+    else if (pk & kCostSym)
+      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
+                                                    xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
+                                                    S.du_sq, cost, alpha);
     else
-      __builtin_unreachable();
-  } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
-    win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T}, nullptr,
-                                    nullptr, xcur, nullptr, bd, decay, max_ls, gr,
-                                    xsa, nullptr, xsb, nullptr, S.du_sq,
-                                    cost, alpha);
-  else if (pk & kCostSym)
-    win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
-                                    xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost, alpha);
-  else
-    win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, first ? S.Cpk : nullptr,
-                                    first && S.Cpk ? S.cost_sym : nullptr, xcur, nullptr, bd,
-                                    decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost, alpha);
+      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, nullptr, nullptr, xcur, nullptr, bd,
+                                                    decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
+                                                    alpha);
+  }
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
   S.alpha[b] = alpha;
@@ -2384,17 +2393,18 @@ int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float*
           T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim,
           G, st);
   } else {
+#define LAUNCH_IT(BM_, LG_, FIRST_, LDS_)                                                                   \
+  k_mpc_iterate<MD, BM_, LG_, FIRST_><<<grid_for(B), kBlock, LDS_, S(stream)>>>(                             \
+      T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, lim, \
+      G, st)
 #define LAUNCH_MPC(BM_)                                                                                      \
   do {                                                                                                       \
     const size_t lds = (size_t)T * kBlock * (MD::N * MD::M + MD::M) * sizeof(float);                        \
-    if (lds * 4 <= kLdsPerCU && !kNoLdsGains)                                                                \
-      k_mpc_iterate<MD, BM_, true><<<grid_for(B), kBlock, lds, S(stream)>>>(                                 \
-          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, \
-          lim, G, st);                                                                                       \
-    else                                                                                                     \
-      k_mpc_iterate<MD, BM_, false><<<grid_for(B), kBlock, 0, S(stream)>>>(                                  \
-          T, B, theta, x_init, C, c, bd, linesearch_decay, max_linesearch_iter, iteration, best_cost_eps, eps, \
-          lim, G, st);                                                                                       \
+    const bool lg = lds * 4 <= kLdsPerCU && !kNoLdsGains;                                                   \
+    if (iteration == 0 && lg) LAUNCH_IT(BM_, true, true, lds);                                               \
+    else if (iteration == 0) LAUNCH_IT(BM_, false, true, 0);                                                 \
+    else if (lg) LAUNCH_IT(BM_, true, false, lds);                                                           \
+    else LAUNCH_IT(BM_, false, false, 0);                                                                    \
   } while (0)
     MODEL_SWITCH_TPP(model, ({
       if (bounds.mode == DILQR_BOUNDS_TENSOR) LAUNCH_MPC(DILQR_BOUNDS_TENSOR);
@@ -2402,6 +2412,7 @@ int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float*
       else LAUNCH_MPC(DILQR_BOUNDS_NONE);
     }));
 #undef LAUNCH_MPC
+#undef LAUNCH_IT
   }
   return launched();
 }

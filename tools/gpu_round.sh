@@ -26,6 +26,11 @@ if [[ "$STEPS" == *all* || "$STEPS" == *prof* ]]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof -o run --output-format csv -- \
       python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $R/$OUT/prof.log 2>&1; rc=$?
   echo "rocprof rc=$rc"; tail -3 $R/$OUT/prof.log; [ $rc -eq 0 ] || exit $rc
+  # the roofline kernel alone (bench --kernels-only: the steady-state fused
+  # iteration's launches are exactly the ones bench.py times with HIP events)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_k -o run --output-format csv -- \
+      python3 $R/bench.py --kernels-only > $R/$OUT/prof_k.log 2>&1; rc=$?
+  echo "rocprof kernels-only rc=$rc"; tail -1 $R/$OUT/prof_k.log; [ $rc -eq 0 ] || exit $rc
   cd $R
 fi
 echo ALL_DONE
