@@ -784,9 +784,15 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
                     const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd, float decay,
                     int max_ls, const GainRecs& ws, float* __restrict__ xa_out,
                     float* __restrict__ ua_out, float* __restrict__ xb_out, float* __restrict__ ub_out,
-                    float* __restrict__ du_sq, float old_cost, float& cost_out, float& alpha_out) {
+                    float* __restrict__ du_sq, float old_cost, float& cost_out, float& alpha_out,
+                    bool b_in_gains = false) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
   constexpr int GREC = m * n + m;                    // gain record: K, k (component-major)
+  // b_in_gains (one round of candidates, gain records in LDS): candidate B's
+  // record t overwrites gain record t, consumed by then (m = 1: both are d
+  // floats), and only the problems whose B wins copy it to xb_out at the end —
+  // instead of every problem writing both candidates to HBM.
+  static_assert(TL != TRAJ_REC || GREC == d, "B records in the gain slots need m = 1");
   float alpha = 1.f, cost = 0.f;
   int win = 0;
   // Candidates A and B travel as the two components of f2 values: every
@@ -844,7 +850,18 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
 #pragma unroll
           for (int i = 0; i < n; ++i) { xa[i] = xp[i].x; xb[i] = xp[i].y; }
           st_xu<TL>(xa_out, nullptr, xa, ua, t, B, b);
-          if (twoB) st_xu<TL>(xb_out, nullptr, xb, ub, t, B, b);
+          if (twoB) {
+            if (b_in_gains) {
+              float rb[d];
+#pragma unroll
+              for (int i = 0; i < n; ++i) rb[i] = xb[i];
+#pragma unroll
+              for (int a = 0; a < m; ++a) rb[n + a] = ub[a];
+              SoaRec<d>::store(ws.p, rb, T, t, ws.B, ws.b);
+            } else {
+              st_xu<TL>(xb_out, nullptr, xb, ub, t, B, b);
+            }
+          }
         } else {
           st(ua_out + ((size_t)t * B + b) * m, ua);
           if (twoB) st(ub_out + ((size_t)t * B + b) * m, ub);
@@ -891,6 +908,19 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
     if (!(cB > old_cost) || p + 1 == max_ls - 1) { cost = cB; alpha = aB; win = 1; break; }
     alpha = aB * decay;                                     // lqr_step_explicit.py:249
   }
+  if constexpr (TL == TRAJ_REC) {
+    if (b_in_gains && win == 1) {                           // B won: its records from LDS to its slot
+      for (int t = 0; t < T; ++t) {
+        float rb[d], xt[n], ut[m];
+        SoaRec<d>::load(rb, ws.p, T, t, ws.B, ws.b);
+#pragma unroll
+        for (int i = 0; i < n; ++i) xt[i] = rb[i];
+#pragma unroll
+        for (int a = 0; a < m; ++a) ut[a] = rb[n + a];
+        st_xu<TL>(xb_out, nullptr, xt, ut, t, B, b);
+      }
+    }
+  }
   cost_out = cost;
   alpha_out = alpha;
   return win;
@@ -911,7 +941,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
                      const GainRecs& ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
                      float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
-                     float& cost_out, float& alpha_out) {
+                     float& cost_out, float& alpha_out, bool b_in_gains = false) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
   constexpr int MODE = BM == DILQR_BOUNDS_NONE ? GAIN_UNC : GAIN_BOX;
   constexpr int GREC = m * n + m;                    // gain record: K, k (component-major)
@@ -1012,11 +1042,11 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       CostDiagConst<d> cc;
       cc.set(pk_last);
       return line_search<Model, BM, TL>(T, B, b, md, x_init, cc, x, u, bd, decay, max_ls, ws, xa_out, ua_out,
-                                         xb_out, ub_out, du_sq, old_cost, cost_out, alpha_out);
+                                         xb_out, ub_out, du_sq, old_cost, cost_out, alpha_out, b_in_gains);
     }
   }
   return line_search<Model, BM, TL>(T, B, b, md, x_init, cs, x, u, bd, decay, max_ls, ws, xa_out, ua_out, xb_out,
-                                     ub_out, du_sq, old_cost, cost_out, alpha_out);
+                                     ub_out, du_sq, old_cost, cost_out, alpha_out, b_in_gains);
 }
 
 template <class Model, int BM>
@@ -1113,10 +1143,13 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   // symmetric, reading only diag(C_t) and c_t when they are all diagonal too
   // (per-lane flags; a wave normally takes one side of the branch)
   const CostFull<n + m> full{C, c};
+  // one round of line-search candidates: B's records go to the consumed gain
+  // slots in LDS and only B-winners copy them out (line_search)
+  const bool b_lds = LG && max_ls <= 2;
   if constexpr (FIRST) {
     win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, S.Cpk, S.Cpk ? S.cost_sym : nullptr,
                                                   xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
-                                                  S.du_sq, cost, alpha);
+                                                  S.du_sq, cost, alpha, b_lds);
   } else {
     const unsigned char pk = S.Cpk ? S.cost_sym[b] : 0;
     if ((pk & (kCostDiag | kCostTinv)) == (kCostDiag | kCostTinv)) {
@@ -1125,7 +1158,7 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
         cc.init(S.Cpk, T, B, b);
         win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd,
                                                       decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
-                                                      alpha);
+                                                      alpha, b_lds);
       } else {
         __builtin_unreachable();
       }
@@ -1133,21 +1166,21 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
       if constexpr (packed_diag_ok<n + m>())
         win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr,
                                                       nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb,
-                                                      nullptr, S.du_sq, cost, alpha);
+                                                      nullptr, S.du_sq, cost, alpha, b_lds);
       else
         __builtin_unreachable();
     } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
       win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T},
                                                     nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr,
-                                                    xsb, nullptr, S.du_sq, cost, alpha);
+                                                    xsb, nullptr, S.du_sq, cost, alpha, b_lds);
     else if (pk & kCostSym)
       win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
                                                     xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
-                                                    S.du_sq, cost, alpha);
+                                                    S.du_sq, cost, alpha, b_lds);
     else
       win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, nullptr, nullptr, xcur, nullptr, bd,
                                                     decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
-                                                    alpha);
+                                                    alpha, b_lds);
   }
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
