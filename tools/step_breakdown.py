@@ -21,13 +21,14 @@ from dilqr import ops  # noqa: E402
 dev = torch.device("cuda", 0)
 T, n, m = bench.T_HORIZON, bench.N_STATE, bench.N_CTRL
 B = int(sys.argv[1]) if len(sys.argv) > 1 else bench.B_PER_GPU
+LIM = float(sys.argv[2]) if len(sys.argv) > 2 else None          # box +-LIM (config 4), default none
 x0n, q, p = bench.make_problems(B)
 x0 = torch.tensor(x0n, device=dev)
 C = torch.diag(torch.tensor(q)).repeat(T, B, 1, 1).to(dev).contiguous()
 c = torch.tensor(p).repeat(T, B, 1).to(dev).contiguous()
 theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
 sv = ops.MPCSolve(T, B, n, m, dev)
-nb, _ = N.make_bounds(None, None)
+nb, _keep = N.make_bounds(None if LIM is None else -LIM, LIM)
 s = N.stream(dev)
 stream = torch.cuda.current_stream(dev)
 ITERS, SOLVES = 10, 6
@@ -73,5 +74,7 @@ out = {k: float(np.mean(v)) for k, v in res.items()}
 out["per_iteration_of_solve"] = out["solve"] / ITERS
 out["solve_iterate"] = float(np.mean([a.elapsed_time(b_) for a, b_ in whole[1:]]))
 out["per_iteration_iterate"] = out["solve_iterate"] / ITERS
+out["mean_best_cost"] = float(sv.best_cost.mean())
 out["B"] = B
+out["box"] = LIM
 print(json.dumps(out))
