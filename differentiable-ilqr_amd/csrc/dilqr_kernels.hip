@@ -1122,13 +1122,17 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
                                                         int iteration, float best_cost_eps, float eps,
                                                         int not_improved_lim, int G, MpcState S) {
   constexpr int n = Model::N, m = Model::M;
-  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   constexpr bool first = FIRST;                             // == (iteration == 0), chosen by the host
   int b = blockIdx.x * blockDim.x + threadIdx.x;
+  // the problem's slot indices and cost flags are read together with the stop
+  // rule's inputs (one memory latency in the prologue, not three)
+  const int bl = b < B ? b : B - 1;
+  const int cur = S.slot[bl], best = S.slot[B + bl];
+  const unsigned char pk = (!FIRST && S.Cpk) ? S.cost_sym[bl] : 0;
+  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   if (b >= B) return;
   Model md; md.load(theta);
   const size_t TBd = (size_t)T * B * (n + m);               // one slot: [T,B,d] records
-  const int cur = S.slot[b], best = S.slot[B + b];
   int sa, sb;
   free_slots(cur, best, sa, sb);
   const float* xcur = S.Xs + cur * TBd;
@@ -1151,7 +1155,6 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
                                                   xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
                                                   S.du_sq, cost, alpha, b_lds);
   } else {
-    const unsigned char pk = S.Cpk ? S.cost_sym[b] : 0;
     if ((pk & (kCostDiag | kCostTinv)) == (kCostDiag | kCostTinv)) {
       if constexpr (packed_diag_ok<n + m>()) {
         CostDiagConst<n + m> cc;
@@ -1370,30 +1373,66 @@ __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iterat
 // for iteration k-1.  Returns true when the solve has stopped (the wave exits).
 DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim) {
   if (k == 0) return false;                            // S_0: begin zeroed ctrl[0..1]
+  // Every load is issued before the first is waited on — the control word and
+  // all partials (valid memory whether or not the solve stopped) — so the
+  // prologue costs one memory latency; the partials go in as uint4 when the
+  // planes are 16-byte aligned (B % 256 == 0).
+  const int gm = sync_gmax(B), par = (k - 1) & 1;
+  const unsigned* pm = S.done_counter + 16 + (2 * par) * gm;
+  const unsigned* pa = S.done_counter + 16 + (2 * par + 1) * gm;
+  const int lane = threadIdx.x & 63;
   const dilqr_mpc_ctrl in = S.ctrl[(k - 1) & 1];        // S_{k-1}
-  dilqr_mpc_ctrl out = in;
-  if (!in.stopped) {
-    const int gm = sync_gmax(B), par = (k - 1) & 1;
-    const unsigned* pm = S.done_counter + 16 + (2 * par) * gm;
-    const unsigned* pa = S.done_counter + 16 + (2 * par + 1) * gm;
-    const int lane = threadIdx.x & 63;
-    unsigned mx = 0u;
-    int any = 0;
+  unsigned mx = 0u;
+  int any = 0;
+  if ((gm & 3) == 0 && G <= 1024) {
+    const uint4* pm4 = reinterpret_cast<const uint4*>(pm);
+    const uint4* pa4 = reinterpret_cast<const uint4*>(pa);
+    uint4 vm[4], va[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = lane + 64 * j;
+      const bool ok = 4 * i < G;
+      vm[j] = ok ? pm4[i] : make_uint4(0u, 0u, 0u, 0u);
+      va[j] = ok ? pa4[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i0 = 4 * (lane + 64 * j);
+      const unsigned e[4] = {vm[j].x, vm[j].y, vm[j].z, vm[j].w};
+      const unsigned f[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (i0 + q < G) {
+          mx = e[q] > mx ? e[q] : mx;
+          any |= (int)f[q];
+        }
+      }
+    }
+  } else {
     for (int i = lane; i < G; i += 64) {
       unsigned v = pm[i];
       mx = v > mx ? v : mx;
       any |= (int)pa[i];
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      unsigned o = __shfl_xor(mx, off, 64);
-      mx = o > mx ? o : mx;
-      any |= __shfl_xor(any, off, 64);
-    }
+  }
+  dilqr_mpc_ctrl out = in;
+  if (!in.stopped) {
+    // wave-uniform decisions by ballot: max < eps <=> every lane's max < eps
+    // (fdn >= 0, so uint order is float order; a NaN fails `< eps` in its lane
+    // as it fails it as the max)
+    const bool all_below = __ballot(!(__uint_as_float(mx) < eps)) == 0ull;
+    const bool any_imp = __ballot(any != 0) != 0ull;
     out.iter = in.iter + 1;
-    out.n_not_improved = any ? 0 : in.n_not_improved + 1;     // mpc_explicit.py:264, 279
-    out.max_du_bits = mx;
-    if (__uint_as_float(mx) < eps || out.n_not_improved > not_improved_lim) out.stopped = 1;   // 297-299
+    out.n_not_improved = any_imp ? 0 : in.n_not_improved + 1;     // mpc_explicit.py:264, 279
+    if (all_below || out.n_not_improved > not_improved_lim) out.stopped = 1;   // 297-299
+    if (blockIdx.x == 0) {                              // the published max (informational)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        unsigned o = __shfl_xor(mx, off, 64);
+        mx = o > mx ? o : mx;
+      }
+      out.max_du_bits = mx;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) S.ctrl[k & 1] = out;
   return out.stopped != 0;
