@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         if (r < n) {
           float xx[n], Dr[d], ft[p];
           D2::xx_row(r, theta, xt, ut, xx);
-          md.jac_row(r, xt, ut, Dr);
+          md.template jac_row<false>(r, xt, ut, Dr);
           D2::xth_row(r, theta, xt, ut, ft);
           float A[n];
 #pragma unroll
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         D2::mcol(r, theta, xt, ut, lam1, Mc);
         if (r < n) {
           float Fr[d];
-          md.jac_row(r, xt, ut, Fr);
+          md.template jac_row<false>(r, xt, ut, Fr);
 #pragma unroll
           for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
         }
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         __syncthreads();
         if (r < n) {
           float Dr[d];
-          md.jac_row(r, xt, ut, Dr);
+          md.template jac_row<false>(r, xt, ut, Dr);
           float s = 0.f;
 #pragma unroll
           for (int j = 0; j < d; ++j) s += Dr[j] * I.vec[j];
@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         D2::mp_row(r, theta, xt, ut, lam1, Mp);
         if (r < n) {
           float Fr[d];
-          md.jac_row(r, xt, ut, Fr);
+          md.template jac_row<false>(r, xt, ut, Fr);
 #pragma unroll
           for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
         }

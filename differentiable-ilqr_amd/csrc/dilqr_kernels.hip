@@ -1226,7 +1226,7 @@ __global__ void __launch_bounds__(64) k_ilqr_iterate_group(int T, int B, const f
 }
 
 template <class Model, int MODE>
-__global__ void __launch_bounds__(64) k_mpc_iterate_group(int T, int B, const float* __restrict__ theta,
+__global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_mpc_iterate_group(int T, int B, const float* __restrict__ theta,
                                                           const float* __restrict__ x_init,
                                                           const float* __restrict__ C, const float* __restrict__ c,
                                                           Bounds bd, float decay, int max_ls, int iteration,

@@ -184,21 +184,27 @@ struct Rocket {
   };
 
   // derivative of state component r (rocket.py:94-156), contraction off so the
-  // rounding follows the reference's eager ops
+  // rounding follows the reference's eager ops — except that the three
+  // divisions by the mass are products with one reciprocal, formed per call
+  // (in the 16-lane kernels every lane's row is a different case of the
+  // switch, so a wave executes all of them; the reciprocal is not kept live
+  // across the kernel: four more live VGPRs cost those kernels an occupancy
+  // step)
   DEV float deriv(int r, const float (&x)[N], const float (&u)[M]) const {
 #pragma clang fp contract(off)
     const float q0 = x[6], q1 = x[7], q2 = x[8], q3 = x[9], wx = x[10], wy = x[11], wz = x[12];
+    const float im = 1.f / mass;
     const float Tx = fminf(fmaxf(u[0], -400.f), 400.f);
     const float Ty = fminf(fmaxf(u[1], -400.f), 400.f);
     const float Tz = fminf(fmaxf(u[2], -400.f), 400.f);
     switch (r) {
       case 0: case 1: case 2: return x[3 + r];
       case 3: return (((1.f - 2.f * (q2 * q2 + q3 * q3)) * Tx + 2.f * (q1 * q2 - q0 * q3) * Ty) +
-                      2.f * (q1 * q3 + q0 * q2) * Tz) / mass + -10.f;
+                      2.f * (q1 * q3 + q0 * q2) * Tz) * im + -10.f;
       case 4: return ((2.f * (q1 * q2 + q0 * q3) * Tx + (1.f - 2.f * (q1 * q1 + q3 * q3)) * Ty) +
-                      2.f * (q2 * q3 - q0 * q1) * Tz) / mass + 0.f;
+                      2.f * (q2 * q3 - q0 * q1) * Tz) * im + 0.f;
       case 5: return ((2.f * (q1 * q3 - q0 * q2) * Tx + 2.f * (q2 * q3 + q0 * q1) * Ty) +
-                      (1.f - 2.f * (q1 * q1 + q2 * q2)) * Tz) / mass + 0.f;
+                      (1.f - 2.f * (q1 * q1 + q2 * q2)) * Tz) * im + 0.f;
       case 6: return 0.5f * (((-wx * q1) + (-wy * q2)) + (-wz * q3));
       case 7: return 0.5f * (((wx * q0) + (wz * q2)) + (-wy * q3));
       case 8: return 0.5f * (((wy * q0) + (-wz * q1)) + (wx * q3));
@@ -220,9 +226,17 @@ struct Rocket {
     return x[r] + deriv(r, x, u) * DT;
   }
 
-  // row r of get_linear_dyn (rocket.py:324-426), unclamped u
+  // row r of get_linear_dyn (rocket.py:324-426), unclamped u.  RECIP: the
+  // divisions by the mass and by J are products with reciprocals formed per
+  // call (27 divisions over the 13 cases a 16-lane group executes -> 4); the
+  // implicit backward keeps the divisions (the reciprocals' live ranges cost
+  // its register-capped kernel more spills than the divisions cost, +7 %).
+  template <bool RECIP = true>
   DEV void jac_row(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M]) const {
     const float dt = DT;
+    const float im = RECIP ? 1.f / mass : 1.f;
+    const auto by_mass = [&](float v) { return RECIP ? v * im : v / mass; };
+    const auto by = [](float v, float Jd, float ij) { return RECIP ? v * ij : v / Jd; };
     const float q0 = x[6], q1 = x[7], q2 = x[8], q3 = x[9], wx = x[10], wy = x[11], wz = x[12];
     const float ux = u[0], uy = u[1], uz = u[2];
 #pragma unroll
@@ -230,31 +244,31 @@ struct Rocket {
     switch (r) {
       case 0: case 1: case 2: D[r + 3] = dt; break;
       case 3:
-        D[6] = dt * (uz * 2 * q2 - uy * 2 * q3) / mass;
-        D[7] = dt * (uy * 2 * q2 + uz * 2 * q3) / mass;
-        D[8] = dt * (uy * 2 * q1 - ux * 4 * q2 + uz * 2 * q0) / mass;
-        D[9] = dt * (uz * 2 * q1 - ux * 4 * q3 - uy * 2 * q0) / mass;
-        D[13] = dt * (1 - 2 * (q2 * q2 + q3 * q3)) / mass;
-        D[14] = dt * 2 * (q1 * q2 - q0 * q3) / mass;
-        D[15] = dt * 2 * (q1 * q3 + q0 * q2) / mass;
+        D[6] = by_mass(dt * (uz * 2 * q2 - uy * 2 * q3));
+        D[7] = by_mass(dt * (uy * 2 * q2 + uz * 2 * q3));
+        D[8] = by_mass(dt * (uy * 2 * q1 - ux * 4 * q2 + uz * 2 * q0));
+        D[9] = by_mass(dt * (uz * 2 * q1 - ux * 4 * q3 - uy * 2 * q0));
+        D[13] = by_mass(dt * (1 - 2 * (q2 * q2 + q3 * q3)));
+        D[14] = by_mass(dt * 2 * (q1 * q2 - q0 * q3));
+        D[15] = by_mass(dt * 2 * (q1 * q3 + q0 * q2));
         break;
       case 4:
-        D[6] = dt * (ux * 2 * q3 - uz * 2 * q1) / mass;
-        D[7] = dt * (ux * 2 * q2 - uy * 4 * q1 - uz * 2 * q0) / mass;
-        D[8] = dt * (ux * 2 * q1 + uz * 2 * q3) / mass;
-        D[9] = dt * (ux * 2 * q0 - uy * 4 * q3 + uz * 2 * q2) / mass;
-        D[13] = dt * 2 * (q1 * q2 + q0 * q3) / mass;
-        D[14] = dt * (1 - 2 * (q1 * q1 + q3 * q3)) / mass;
-        D[15] = dt * 2 * (q2 * q3 - q0 * q1) / mass;
+        D[6] = by_mass(dt * (ux * 2 * q3 - uz * 2 * q1));
+        D[7] = by_mass(dt * (ux * 2 * q2 - uy * 4 * q1 - uz * 2 * q0));
+        D[8] = by_mass(dt * (ux * 2 * q1 + uz * 2 * q3));
+        D[9] = by_mass(dt * (ux * 2 * q0 - uy * 4 * q3 + uz * 2 * q2));
+        D[13] = by_mass(dt * 2 * (q1 * q2 + q0 * q3));
+        D[14] = by_mass(dt * (1 - 2 * (q1 * q1 + q3 * q3)));
+        D[15] = by_mass(dt * 2 * (q2 * q3 - q0 * q1));
         break;
       case 5:
-        D[6] = dt * (uy * 2 * q1 - ux * 2 * q2) / mass;
-        D[7] = dt * (ux * 2 * q3 + uy * 2 * q0 - uz * 4 * q1) / mass;
-        D[8] = dt * (uy * 2 * q3 - ux * 2 * q0 - uz * 4 * q2) / mass;
-        D[9] = dt * (ux * 2 * q1 + uy * 2 * q2) / mass;
-        D[13] = dt * 2 * (q1 * q3 - q0 * q2) / mass;
-        D[14] = dt * 2 * (q2 * q3 + q0 * q1) / mass;
-        D[15] = dt * (1 - 2 * (q1 * q1 + q2 * q2)) / mass;
+        D[6] = by_mass(dt * (uy * 2 * q1 - ux * 2 * q2));
+        D[7] = by_mass(dt * (ux * 2 * q3 + uy * 2 * q0 - uz * 4 * q1));
+        D[8] = by_mass(dt * (uy * 2 * q3 - ux * 2 * q0 - uz * 4 * q2));
+        D[9] = by_mass(dt * (ux * 2 * q1 + uy * 2 * q2));
+        D[13] = by_mass(dt * 2 * (q1 * q3 - q0 * q2));
+        D[14] = by_mass(dt * 2 * (q2 * q3 + q0 * q1));
+        D[15] = by_mass(dt * (1 - 2 * (q1 * q1 + q2 * q2)));
         break;
       case 6:
         D[7] = -dt * 0.5f * wx; D[8] = -dt * 0.5f * wy; D[9] = -dt * 0.5f * wz;
@@ -272,17 +286,23 @@ struct Rocket {
         D[6] = dt * 0.5f * wz; D[7] = dt * 0.5f * wy; D[8] = -dt * 0.5f * wx;
         D[10] = -dt * 0.5f * q2; D[11] = dt * 0.5f * q1; D[12] = dt * 0.5f * q0;
         break;
-      case 10:
-        D[11] = -dt * (wz * Jz - wz * Jy) / Jx; D[12] = -dt * (wy * Jz - wy * Jy) / Jx;
+      case 10: {
+        const float ij = RECIP ? 1.f / Jx : 1.f;
+        D[11] = by(-dt * (wz * Jz - wz * Jy), Jx, ij); D[12] = by(-dt * (wy * Jz - wy * Jy), Jx, ij);
         break;
-      case 11:
-        D[10] = -dt * (wz * Jx - wz * Jz) / Jy; D[12] = -dt * (wx * Jx - wx * Jz) / Jy;
-        D[15] = dt * (l / 2) / Jy;
+      }
+      case 11: {
+        const float ij = RECIP ? 1.f / Jy : 1.f;
+        D[10] = by(-dt * (wz * Jx - wz * Jz), Jy, ij); D[12] = by(-dt * (wx * Jx - wx * Jz), Jy, ij);
+        D[15] = by(dt * (l / 2), Jy, ij);
         break;
-      default:  // 12
-        D[10] = -dt * (wy * Jy - wy * Jx) / Jz; D[11] = -dt * (wx * Jy - wx * Jx) / Jz;
-        D[14] = -dt * (l / 2) / Jz;
+      }
+      default: {  // 12
+        const float ij = RECIP ? 1.f / Jz : 1.f;
+        D[10] = by(-dt * (wy * Jy - wy * Jx), Jz, ij); D[11] = by(-dt * (wx * Jy - wx * Jx), Jz, ij);
+        D[14] = by(-dt * (l / 2), Jz, ij);
         break;
+      }
     }
   }
 
