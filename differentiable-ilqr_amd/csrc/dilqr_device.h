@@ -77,8 +77,10 @@ DEV void sincos_poly(S r, S& s1, S& c1) {
   c1 = vfma(vfma(vfma(S(2.443315711809948e-5f), z, S(-1.388731625493765e-3f)), z, S(4.166664568298827e-2f)),
             z * z, S(-0.5f) * z) + S(1.0f);
 }
+// The reduction-and-polynomial path runs unconditionally (branch-free);
+// lanes whose argument is out of its range are patched afterwards in a branch
+// that a wave skips when none of its lanes needs it.
 DEV void sincos_fast(float d, float& s, float& c) {
-  if (!(fabsf(d) <= 8192.f)) { sincosf(d, &s, &c); return; }
   const float k = __builtin_rintf(d * 0.636619772f);
   float r = vfma(-k, 1.5703125f, d);
   r = vfma(-k, 4.837512969970703125e-4f, r);
@@ -86,15 +88,9 @@ DEV void sincos_fast(float d, float& s, float& c) {
   float s1, c1;
   sincos_poly(r, s1, c1);
   sincos_quadrant((int)k, s1, c1, s, c);
+  if (__builtin_expect(!(fabsf(d) <= 8192.f), 0)) sincosf(d, &s, &c);
 }
 DEV void sincos_fast(f2 d, f2& s, f2& c) {
-  if (!(fabsf(d.x) <= 8192.f) || !(fabsf(d.y) <= 8192.f)) {
-    float s0, c0, s1, c1;
-    sincos_fast(d.x, s0, c0);
-    sincos_fast(d.y, s1, c1);
-    s = f2{s0, s1}; c = f2{c0, c1};
-    return;
-  }
   const f2 k = f2{__builtin_rintf(d.x * 0.636619772f), __builtin_rintf(d.y * 0.636619772f)};
   f2 r = vfma(-k, f2(1.5703125f), d);
   r = vfma(-k, f2(4.837512969970703125e-4f), r);
@@ -104,6 +100,10 @@ DEV void sincos_fast(f2 d, f2& s, f2& c) {
   float sa, ca, sb, cb;
   sincos_quadrant((int)k.x, s1.x, c1.x, sa, ca);
   sincos_quadrant((int)k.y, s1.y, c1.y, sb, cb);
+  if (__builtin_expect(!(fabsf(d.x) <= 8192.f) || !(fabsf(d.y) <= 8192.f), 0)) {
+    if (!(fabsf(d.x) <= 8192.f)) sincosf(d.x, &sa, &ca);
+    if (!(fabsf(d.y) <= 8192.f)) sincosf(d.y, &sb, &cb);
+  }
   s = f2{sa, sb}; c = f2{ca, cb};
 }
 
