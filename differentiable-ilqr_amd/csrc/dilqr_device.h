@@ -524,7 +524,10 @@ struct RiccatiState {
     }
 
     if constexpr (MODE == GAIN_UNC && M == 1) {          // lqr_step_explicit.py:86-88
-      float r = 1.0f / Quu[0][0];
+      // v_rcp_f32 (1 ulp) instead of the correctly rounded 1/Q_uu, whose IEEE
+      // division expands to ~10 instructions (div_scale/fmas/fixup) per step;
+      // the reference's -Q_ux/Q_uu and this -(r*Q_ux) differ by rounding either way
+      float r = __builtin_amdgcn_rcpf(Quu[0][0]);
 #pragma unroll
       for (int j = 0; j < N; ++j) K[0][j] = -(r * Q[N][j]);
       k[0] = -(r * qu[0]);

@@ -20,6 +20,25 @@ constexpr bool kNoLdsGains = DILQR_NO_LDS_GAINS;   // test builds: gain records 
 
 static inline int grid_for(long long n) { return (int)((n + kBlock - 1) / kBlock); }
 
+// Diagnostic build only (-DDILQR_STAMPS, tools/phase_stamps.py; never the
+// shipped library): lane 0 of every wave of the fused MPC iteration writes
+// s_memtime at its phase boundaries (kernel entry, after the stop-rule
+// prologue, after the sweep, after the line search, exit) and s_memrealtime
+// at entry/exit into a buffer of its own that nothing else reads.
+#ifdef DILQR_STAMPS
+constexpr int kStampSlots = 8, kStampWaves = 4096;
+__device__ unsigned long long g_stamps[kStampWaves * kStampSlots];
+#define DILQR_STAMP(k)                                                                     \
+  do {                                                                                     \
+    const unsigned w_ = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;                     \
+    if ((threadIdx.x & 63u) == 0 && w_ < (unsigned)kStampWaves)                             \
+      g_stamps[w_ * kStampSlots + (k)] = (k) >= 6 ? __builtin_amdgcn_s_memrealtime()       \
+                                                  : __builtin_amdgcn_s_memtime();          \
+  } while (0)
+#else
+#define DILQR_STAMP(k) do {} while (0)
+#endif
+
 DEV float bound_lo(const Bounds& bd, long long idx) { return bd.mode == DILQR_BOUNDS_TENSOR ? bd.lo_t[idx] : bd.lo; }
 DEV float bound_hi(const Bounds& bd, long long idx) { return bd.mode == DILQR_BOUNDS_TENSOR ? bd.hi_t[idx] : bd.hi; }
 }  // namespace dilqr
@@ -536,7 +555,9 @@ DEV void ld_xu(float (&x)[n], float (&u)[m], const float* __restrict__ xp, const
   const size_t tb = t * B + b;
   if constexpr (TL == TRAJ_REC) {
     float r[n + m];
-    ld(r, xp + tb * (n + m));
+    // lane part and (uniform) step part of the address kept apart: the step's
+    // offset is scalar arithmetic, the lane adds it with one 64-bit add
+    ld(r, (xp + (size_t)b * (n + m)) + t * (size_t)B * (n + m));
 #pragma unroll
     for (int i = 0; i < n; ++i) x[i] = r[i];
 #pragma unroll
@@ -780,7 +801,7 @@ constexpr int kPFL = DILQR_PF_LS;                   // the line search's prefetc
 // which is exactly the sequential search.  A wave otherwise pays a whole
 // second latency-bound pass whenever any of its 64 problems backtracks.
 template <class Model, int BM, int TL, class CostT>
-DEV int line_search(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
+DEV int line_search(int T, int B, int b, const Model md, const float* __restrict__ x_init, const CostT& cs,
                     const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd, float decay,
                     int max_ls, const GainRecs& ws, float* __restrict__ xa_out,
                     float* __restrict__ ua_out, float* __restrict__ xb_out, float* __restrict__ ub_out,
@@ -800,7 +821,9 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
   // v_pk_mul_f32 / v_pk_add_f32), and each component rounds exactly like the
   // scalar rollout of that candidate.  (Measured alternatives that were
   // slower on MI355X: unrolling the step loop twice over two prefetch buffers
-  // and making every store unconditional, +3 us per iteration.)
+  // and making every store unconditional, +3 us per iteration; unrolling it
+  // three times with the three prefetch buffers rotating roles instead of
+  // being copied — 13 fewer v_mov per step in the listing — +4 us.)
   for (int p = 0; p < max_ls; p += 2) {
     const bool twoB = p + 1 < max_ls;                       // uniform
     const float aA = alpha, aB = alpha * decay;
@@ -936,7 +959,7 @@ DEV int line_search(int T, int B, int b, const Model& md, const float* __restric
 // the registers holding that record), and a time-invariant diagonal cost is
 // handed to this iteration's line search in registers, so C is read once.
 template <class Model, int BM, int TL, bool ROLLOUT, class CostT>
-DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restrict__ x_init, const CostT& cs,
+DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restrict__ x_init, const CostT& cs,
                      float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
                      const GainRecs& ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
@@ -961,10 +984,15 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
     SweepIn<n, m, TL, BM> cur, n1, n2;
     cur.load(cs, x, u, bd, T - 1, B, b);
     if constexpr (kPF >= 2) n1.load(cs, x, u, bd, T > 1 ? T - 2 : 0, B, b);
-#pragma unroll 2
-    for (int t = T - 1; t >= 0; --t) {
-      if constexpr (kPF >= 2) n2.load(cs, x, u, bd, t > 1 ? t - 2 : 0, B, b);   // prefetch step t-2
-      else n1.load(cs, x, u, bd, t > 0 ? t - 1 : 0, B, b);                       // prefetch step t-1
+    // step T-1 (F = 0, V = 0) is peeled off the loop, so the loop body always
+    // computes the Jacobian (no zero-F defaults materialised at every step;
+    // -1 us per fused iteration).  (Rotating the prefetch buffers by role
+    // through the lambda's arguments instead of copying them measured +6 us.)
+    using SI = SweepIn<n, m, TL, BM>;
+    // one step on the inputs in `cur`: linearise, Riccati, stage cost; the
+    // step's gain record is left in g (the caller stores it)
+    auto sweep_body = [&](int t, auto last_c, const SI& cur, float (&g)[GREC]) {
+      constexpr bool LAST = decltype(last_c)::value;
       float tau[d], Ctau[d], cb[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) tau[i] = cur.x[i];
@@ -973,7 +1001,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
       if (pack_out) {                                   // first iteration: build the packed copy
         float buf[PK];
         pack_cost(cur.C, cur.c, buf, sym, diag);
-        if (t == T - 1) {
+        if constexpr (LAST) {
           SoaRec<PK>::store(pack_out, buf, T, t, B, b);
 #pragma unroll
           for (int k = 0; k < PK; ++k) pk_last[k] = buf[k];
@@ -991,7 +1019,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
 #pragma unroll
       for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + cur.c[i];
       float Ft[n][d];
-      if (t < T - 1) {
+      if constexpr (!LAST) {
         if constexpr (ROLLOUT && Model::kJacFromNext) md.jacobian_next(cur.x, cur.u, xn, Ft);
         else md.jacobian(cur.x, cur.u, Ft);
       } else {
@@ -1018,25 +1046,34 @@ DEV int ilqr_problem(int T, int B, int b, const Model& md, const float* __restri
         if (symsofar) rs.template step<MODE, FS, CostT::kDiag, true>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
         else rs.template step<MODE, FS, CostT::kDiag, false>(cur.C, cb, Ft, zIt, lb, ub, Kt, kt);
       }
-      float g[GREC];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
 #pragma unroll
         for (int j = 0; j < n; ++j) g[a * n + j] = Kt[a][j];
         g[m * n + a] = kt[a];
       }
-      SoaRec<GREC>::store(ws.p, g, T, t, ws.B, ws.b);
       old_cost += obj;          // summed over t = T-1..0 (the reference's torch sum has its own order)
 #pragma unroll
       for (int i = 0; i < n; ++i) xn[i] = cur.x[i];
+    };
+    auto sweep_step = [&](int t, auto last_c) {
+      if constexpr (kPF >= 2) n2.load(cs, x, u, bd, t > 1 ? t - 2 : 0, B, b);   // prefetch step t-2
+      else n1.load(cs, x, u, bd, t > 0 ? t - 1 : 0, B, b);                       // prefetch step t-1
+      float g[GREC];
+      sweep_body(t, last_c, cur, g);
+      SoaRec<GREC>::store(ws.p, g, T, t, ws.B, ws.b);
       cur = n1;
       if constexpr (kPF >= 2) n1 = n2;
-    }
+    };
+    sweep_step(T - 1, std::true_type{});
+#pragma unroll 2
+    for (int t = T - 2; t >= 0; --t) sweep_step(t, std::false_type{});
     if (sym_out)
       sym_out[b] = sym ? (unsigned char)(kCostSym | (diag && packed_diag_ok<d>() ? kCostDiag : 0) |
                                          (tinv ? kCostTinv : 0))
                        : 0;
   }
+  DILQR_STAMP(2);
   if constexpr (!CostT::kDiag && packed_diag_ok<d>()) {
     if (pack_out && sym && diag && tinv) {              // iteration 0 of a diag(q), p over t cost
       CostDiagConst<d> cc;
@@ -1096,16 +1133,15 @@ constexpr int kSlots = 4;
 DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim);
 
 // the two lowest slot indices not in {cur, best}
+// (selects only: the earlier counter-indexed form became a stack array)
 DEV void free_slots(int cur, int best, int& sa, int& sb) {
-  int k = 0;
-  sa = sb = 0;
+  sa = -1;
+  sb = -1;
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) {
-    if (s != cur && s != best) {
-      if (k == 0) sa = s;
-      else if (k == 1) sb = s;
-      ++k;
-    }
+    const bool fr = s != cur && s != best;
+    sb = (fr && sa >= 0 && sb < 0) ? s : sb;
+    sa = (fr && sa < 0) ? s : sa;
   }
 }
 
@@ -1129,8 +1165,11 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   const int bl = b < B ? b : B - 1;
   const int cur = S.slot[bl], best = S.slot[B + bl];
   const unsigned char pk = (!FIRST && S.Cpk) ? S.cost_sym[bl] : 0;
+  DILQR_STAMP(0);
+  DILQR_STAMP(6);
   if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   if (b >= B) return;
+  DILQR_STAMP(1);
   Model md; md.load(theta);
   const size_t TBd = (size_t)T * B * (n + m);               // one slot: [T,B,d] records
   int sa, sb;
@@ -1165,6 +1204,11 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
       } else {
         __builtin_unreachable();
       }
+#ifdef DILQR_ONLY_DIAGCONST                // ISA-listing builds only (tools/loop_stats.py)
+    } else {
+      __builtin_unreachable();
+    }
+#else
     } else if (pk & kCostDiag) {           // set by iteration 0 only when packed_diag_ok
       if constexpr (packed_diag_ok<n + m>())
         win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr,
@@ -1184,7 +1228,9 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
       win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, nullptr, nullptr, xcur, nullptr, bd,
                                                     decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
                                                     alpha, b_lds);
+#endif
   }
+  DILQR_STAMP(3);
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
   S.alpha[b] = alpha;
@@ -1195,6 +1241,8 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   }
   S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
   S.slot[b] = (unsigned char)nw;
+  DILQR_STAMP(4);
+  DILQR_STAMP(7);
 }
 
 // the same two kernels for the 16-lanes-per-problem models (dilqr_group.h)
@@ -2043,6 +2091,15 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
 
 // ====================================================================== C-ABI
 using namespace dilqr;
+
+#ifdef DILQR_STAMPS
+// diagnostic build only: copy the phase stamps of the last fused MPC iteration
+extern "C" int dilqr_debug_stamps(unsigned long long* host, int n) {
+  if (n > kStampWaves * kStampSlots) n = kStampWaves * kStampSlots;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0 : -1;
+}
+#endif
 
 namespace {
 

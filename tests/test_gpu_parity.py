@@ -80,6 +80,42 @@ def test_riccati_sweep_vs_golden(golden, name, variant):
     assert relerr(cpu(k), g[f"{name}_{variant}k"]) < 1e-4
 
 
+@pytest.mark.parametrize("n,m", [(5, 1), (3, 1), (4, 2)])
+@pytest.mark.parametrize("with_x,box", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("T", [1, 9])
+def test_sweep_batch_size_independent(n, m, with_x, box, T):
+    """Problems are independent in the Riccati sweep (lqr_step_explicit.py:54-162
+    is batch-independent): the same problems at B = 128
+    (whole waves) and as the first 128 of B = 129 (a partial last wave) give
+    bit-identical K, k and pnqp counts.  Every third problem has an asymmetric
+    C (the non-SYM step).  (Guards any B-dependent kernel path, such as the
+    LDS-DMA-staged sweep that was measured and rejected)"""
+    from dilqr import ops
+    g = torch.Generator().manual_seed(11)
+    d, B0, B1 = n + m, 129, 128
+    L = torch.randn(T, B0, d, d, generator=g) * (0.5 / d ** 0.5)
+    C = L @ L.transpose(-1, -2) + 0.1 * torch.eye(d)
+    C[:, ::3, 0, d - 1] += 0.05
+    c = torch.randn(T, B0, d, generator=g)
+    F = None
+    if T > 1:
+        A = torch.eye(n) + 0.05 * torch.randn(T - 1, B0, n, n, generator=g)
+        F = torch.cat([A, 0.1 * torch.randn(T - 1, B0, n, m, generator=g)], -1)
+    kw = {}
+    if with_x:
+        kw = dict(x=torch.randn(T, B0, n, generator=g), u=torch.randn(T, B0, m, generator=g))
+    bnd = dict(u_lower=-0.5, u_upper=0.5) if box else {}
+
+    def run(Bn):
+        sl = lambda t: None if t is None else t[:, :Bn].contiguous().to(DEV)
+        return ops.lqr_backward(sl(C), sl(c), sl(F), n, m, want_nqp=True,
+                                **{k_: sl(v) for k_, v in kw.items()}, **bnd)
+    Ka, ka, qa = run(B1)
+    Kb, kb, qb = run(B0)
+    assert torch.equal(Ka, Kb[:, :B1]) and torch.equal(ka, kb[:, :B1]) and torch.equal(qa, qb[:B1])
+    assert torch.isfinite(Ka).all()
+
+
 def test_riccati_m3_lindx_shape(golden):
     """(n,m)=(4,3): the m>1 gain solve (pinverse == inverse for SPD Q_uu) and the
     Cholesky+1e-6 engine variant."""

@@ -25,6 +25,8 @@ def short(name):
     for key in ("k_mpc_iterate", "k_ilqr_iterate", "k_lqr_backward", "k_mpc_norm_control", "k_implicit_backward",
                 "k_lqr_forward", "k_lqr_adjoint"):
         if key in name:
+            if key == "k_mpc_iterate" and name.split("(")[0].rstrip().endswith("true>"):
+                key += "<first>"                      # iteration 0's own instantiation (FIRST = true)
             return key + ("<box>" if "Li3EE" in name else "")
     return None
 
@@ -72,4 +74,4 @@ def main(pmc_dir, round_tag):
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc"),
-         sys.argv[2] if len(sys.argv) > 2 else "r01")
+         sys.argv[2] if len(sys.argv) > 2 else "r02")
