@@ -107,6 +107,11 @@ def _timed_solves(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, lqr_iter
 
     def solve():
         sv.begin(model_id, theta, x0)
+        if sv.fixed_iters == lqr_iter:                  # the stop rule cannot fire: fixed-count solve
+            for i in range(lqr_iter):
+                sv.iterate_fixed(model_id, theta, x0, C, c, bounds, decay, max_ls, i, 1e-4)
+            sv.finish_fixed(lqr_iter)
+            return
         for i in range(lqr_iter):
             sv.iterate(model_id, theta, x0, C, c, bounds, decay, max_ls, i, 1e-4, 0.0, 10 ** 9)
     for _ in range(warmup_solves):
@@ -230,7 +235,7 @@ def secondary_configs(dev):
     C = torch.diag(q).repeat(T, B, 1, 1).to(dev).contiguous()
     c = p.repeat(T, B, 1).to(dev).contiguous()
     theta = ops.theta_of(dx, x0)
-    sv = ops.MPCSolve(T, B, n, m, dev)
+    sv = ops.MPCSolve(T, B, n, m, dev, fixed_iters=10)
     nb, _ = N.make_bounds(None, None)
     val, ms_it = _timed_solves(sv, N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, 10, 2, 1)
     sv.begin(N.MODEL_ROCKET, theta, x0)
@@ -268,7 +273,7 @@ def secondary_configs(dev):
     C = torch.diag(torch.tensor(qn)).repeat(T, B, 1, 1).to(dev).contiguous()
     c = torch.tensor(pn).repeat(T, B, 1).to(dev).contiguous()
     theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
-    sv = ops.MPCSolve(T, B, n, m, dev)
+    sv = ops.MPCSolve(T, B, n, m, dev, fixed_iters=10)
     for lim in (100.0, 10.0):
         bd, keep = N.make_bounds(-lim, lim)
         val, ms_it = _timed_solves(sv, N.MODEL_CARTPOLE, theta, x0, C, c, bd, 0.5, 2, 10, 3, 1)
@@ -363,7 +368,10 @@ def main():
     C = torch.diag(torch.tensor(q)).repeat(T_HORIZON, B, 1, 1).to(dev).contiguous()     # materialised per (t,b)
     c = torch.tensor(p).repeat(T_HORIZON, B, 1).to(dev).contiguous()
     theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
-    sv = ops.MPCSolve(T_HORIZON, B, N_STATE, N_CTRL, dev)
+    # eps = 0 and not_improved_lim = 1e9: the stop rule cannot fire, so the
+    # solve is a fixed-count one (ops.mpc_solve takes the same path): one launch
+    # per iteration, best_du formed by finish_fixed at the end of each solve
+    sv = ops.MPCSolve(T_HORIZON, B, N_STATE, N_CTRL, dev, fixed_iters=args.lqr_iter)
     bounds, _ = N.make_bounds(None, None)
     stream = torch.cuda.current_stream(dev)
     s = N.stream(dev)
@@ -374,7 +382,9 @@ def main():
         it = state["i"] % args.lqr_iter
         if it == 0:
             sv.begin(N.MODEL_CARTPOLE, theta, x0)
-        sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, it, 1e-4, 0.0, 10 ** 9)
+        sv.iterate_fixed(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, it, 1e-4)
+        if it == args.lqr_iter - 1:
+            sv.finish_fixed(args.lqr_iter)
         state["i"] += 1
 
     if args.kernels_only:

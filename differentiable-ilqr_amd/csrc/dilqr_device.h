@@ -82,6 +82,10 @@ DEV void sincos_poly(S r, S& s1, S& c1) {
 // that a wave skips when none of its lanes needs it.
 DEV void sincos_fast(float d, float& s, float& c) {
   const float k = __builtin_rintf(d * 0.636619772f);
+  if (__builtin_amdgcn_ballot_w64(!(k == 0.f)) == 0) {     // |d| <= pi/4 wave-wide: see the f2 form
+    sincos_poly(d, s, c);
+    return;
+  }
   float r = vfma(-k, 1.5703125f, d);
   r = vfma(-k, 4.837512969970703125e-4f, r);
   r = vfma(-k, 7.54978995489188216e-8f, r);
@@ -92,6 +96,13 @@ DEV void sincos_fast(float d, float& s, float& c) {
 }
 DEV void sincos_fast(f2 d, f2& s, f2& c) {
   const f2 k = f2{__builtin_rintf(d.x * 0.636619772f), __builtin_rintf(d.y * 0.636619772f)};
+  // The usual case, |d| <= pi/4 in every lane of the wave (k = 0: the
+  // reduction leaves r = d exactly and the quadrant fix-up is the identity):
+  // the polynomials alone, the same values bit for bit, ~25 fewer instructions.
+  if (__builtin_amdgcn_ballot_w64(!(k.x == 0.f && k.y == 0.f)) == 0) {
+    sincos_poly(d, s, c);
+    return;
+  }
   f2 r = vfma(-k, f2(1.5703125f), d);
   r = vfma(-k, f2(4.837512969970703125e-4f), r);
   r = vfma(-k, f2(7.54978995489188216e-8f), r);

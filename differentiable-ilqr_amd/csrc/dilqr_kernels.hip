@@ -1240,6 +1240,7 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
     S.slot[B + b] = (unsigned char)nw;
   }
   S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
+  if (S.best_iter && (first || better)) S.best_iter[b] = iteration;       // fixed-count solves
   S.slot[b] = (unsigned char)nw;
   DILQR_STAMP(4);
   DILQR_STAMP(7);
@@ -1308,6 +1309,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_mpc_iterate_group(in
       S.slot[B + b] = (unsigned char)nw;
     }
     S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
+    if (S.best_iter && (first || better)) S.best_iter[b] = iteration;     // fixed-count solves
     S.slot[b] = (unsigned char)nw;
   }
 }
@@ -1417,10 +1419,36 @@ __global__ void __launch_bounds__(256) k_mpc_norm_rows(int TM, int B, int iterat
   }
 }
 
+// ---------------- fixed-count solves (eps <= 0 and not_improved_lim >= the
+// iteration count: the stop rule provably never fires, mpc_explicit.py:297-299).
+// No stop-rule launch per iteration: each iteration writes its du rows into its
+// own plane of du_sq ([iters,T,m,B]) and records, per problem, the last
+// iteration that took the best-iterate branch (best_iter).  At the end this
+// kernel forms best_du — the quirk row (lqr_step_explicit.py:245-247) of that
+// iteration, summed in the same order as k_mpc_norm_rows, so the same bits —
+// and publishes the iteration count in both control words.
+__global__ void __launch_bounds__(256) k_mpc_fixed_finish(int TM, int B, int iterations, MpcState S) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < B) {
+    const int k = S.best_iter[r];
+    const float* p = S.du_sq + ((size_t)k * B + r) * TM;
+    float s = 0.f;
+    for (int i = 0; i < TM; ++i) s += p[i];
+    S.best_du[r] = sqrtf(s);
+  }
+  if (r < 2) {
+    dilqr_mpc_ctrl c = S.ctrl[r];
+    c.iter = iterations;
+    c.stopped = 0;
+    S.ctrl[r] = c;
+  }
+}
+
 // Prologue of iteration k >= 1 (one 64-lane wave per workgroup): the stop rule
 // for iteration k-1.  Returns true when the solve has stopped (the wave exits).
 DEV bool mpc_decide(const MpcState& S, int B, int k, int G, float eps, int not_improved_lim) {
   if (k == 0) return false;                            // S_0: begin zeroed ctrl[0..1]
+  if (G < 0) return false;                             // fixed-count solve: the rule cannot fire
   // Every load is issued before the first is waited on — the control word and
   // all partials (valid memory whether or not the solve stopped) — so the
   // prologue costs one memory latency; the partials go in as uint4 when the
@@ -2149,7 +2177,7 @@ inline int launch_norm_rows(int TM, int B, int iteration, const MpcState& st, hi
 
 extern "C" {
 
-int dilqr_version(void) { return 2; }
+int dilqr_version(void) { return 3; }
 
 int dilqr_model_num_ctrl(int model) {
   switch (model) {
@@ -2499,16 +2527,22 @@ int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float
   return launched();
 }
 
-int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
-                       const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
-                       int iteration, float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st,
-                       void* stream) {
+// the fused iteration's launch; fixed: a fixed-count solve (no stop rule,
+// this iteration's du rows into plane `iteration` of du_sq, best_iter kept)
+static int mpc_step(int model, int T, int B, const float* theta, const float* x_init, const float* C, const float* c,
+                    dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter, int iteration,
+                    float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st, bool fixed,
+                    void* stream) {
   if (T < 1 || B < 0 || max_linesearch_iter < 1 || iteration < 0 || !theta || !x_init || !C || !c) return DILQR_E_ARG;
   if (!al16(x_init) || !al16(C) || !al16(c) || bad_state(st) || bad_bounds(bounds)) return DILQR_E_ARG;
+  if (fixed && !st.best_iter) return DILQR_E_ARG;
   if (B == 0) return 0;
   const int m = dilqr_model_num_ctrl(model);
   if (m < 1) return DILQR_E_SHAPE;
-  const int G = norm_geom(T * m, B).blocks;            // partials of the previous iteration's rows
+  // G: partials of the previous iteration's rows; < 0: fixed-count solve
+  const int G = fixed ? -1 : norm_geom(T * m, B).blocks;
+  if (fixed) st.du_sq += (size_t)iteration * T * m * B;
+  else st.best_iter = nullptr;
   const int lim = not_improved_lim;
   Bounds bd = mkb(bounds);
   bool box = bounds.mode != DILQR_BOUNDS_NONE;
@@ -2543,6 +2577,28 @@ int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float*
 #undef LAUNCH_MPC
 #undef LAUNCH_IT
   }
+  return launched();
+}
+
+int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
+                       const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
+                       int iteration, float best_cost_eps, float eps, int not_improved_lim, dilqr_mpc_state st,
+                       void* stream) {
+  return mpc_step(model, T, B, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, iteration,
+                  best_cost_eps, eps, not_improved_lim, st, false, stream);
+}
+
+int dilqr_mpc_iterate_fixed_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
+                                const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
+                                int iteration, float best_cost_eps, dilqr_mpc_state st, void* stream) {
+  return mpc_step(model, T, B, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, iteration,
+                  best_cost_eps, 0.f, 0, st, true, stream);
+}
+
+int dilqr_mpc_finish_fixed_f32(int T, int m, int B, int iterations, dilqr_mpc_state st, void* stream) {
+  if (T < 1 || m < 1 || B < 0 || iterations < 1 || bad_state(st) || !st.best_iter) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  k_mpc_fixed_finish<<<(B + 255) / 256, 256, 0, S(stream)>>>(T * m, B, iterations, st);
   return launched();
 }
 

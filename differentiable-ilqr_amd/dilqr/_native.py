@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must be imported first: libdilqr.so then binds to t
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DILQR_LIB", os.path.join(_HERE, "libdilqr.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 MODEL_LINDX, MODEL_PENDULUM, MODEL_CARTPOLE, MODEL_ROCKET = 0, 1, 2, 3
 BOUNDS_NONE, BOUNDS_SCALAR, BOUNDS_TENSOR = 0, 1, 2
@@ -32,7 +32,7 @@ class MpcState(ctypes.Structure):
     """dilqr_mpc_state: device pointers of one MPC solve (include/dilqr.h)."""
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("Xs", "Us", "slot", "best_cost", "best_du", "improved", "cost", "alpha", "du_sq",
-                 "full_du_norm", "ws", "ctrl", "done_counter", "Cpk", "cost_sym")]
+                 "full_du_norm", "ws", "ctrl", "done_counter", "Cpk", "cost_sym", "best_iter")]
 
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 SIGNATURES = {
@@ -62,6 +62,8 @@ SIGNATURES = {
     "dilqr_mpc_iterate_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
     "dilqr_mpc_step_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState, _vp], _i),
     "dilqr_mpc_stop_rule_f32": ([_i, _i, _i, _i, MpcState, _vp], _i),
+    "dilqr_mpc_iterate_fixed_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, MpcState, _vp], _i),
+    "dilqr_mpc_finish_fixed_f32": ([_i, _i, _i, _i, MpcState, _vp], _i),
     "dilqr_mpc_gather_best_f32": ([_i, _i, _i, _i, MpcState, _vp, _vp, _vp], _i),
     "dilqr_implicit_backward_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _vp, _vp, _vp,
                                      _vp, _vp], _i),

@@ -153,9 +153,14 @@ class MPCSolve:
     slots per problem (current, best, two line-search candidates), per-problem
     best bookkeeping, the loop control block."""
 
-    def __init__(self, T, B, n, m, device, packed_cost=True):
+    def __init__(self, T, B, n, m, device, packed_cost=True, fixed_iters=None):
+        """fixed_iters: a fixed-count solve of that many iterations (the stop rule
+        cannot fire: eps <= 0, not_improved_lim >= iterations) — one launch per
+        iteration (iterate_fixed) and finish_fixed at the end; du_sq keeps one
+        [T,m,B] plane per iteration."""
         dev = device
         self.T, self.B, self.n, self.m = T, B, n, m
+        self.fixed_iters = fixed_iters
         # slots: [4,T,B,n+m] records [x_t; u_t] for the thread-per-problem models
         # (Us aliases Xs, unused by the kernels), the caller's [4,T,B,n] and
         # [4,T,B,m] for rocket
@@ -172,7 +177,8 @@ class MPCSolve:
         self.improved = torch.zeros(B, dtype=torch.int32, device=dev)
         self.cost = torch.empty(B, device=dev)
         self.alpha = torch.empty(B, device=dev)
-        self.du_sq = torch.empty(T, m, B, device=dev)
+        self.du_sq = torch.empty((fixed_iters or 1) * T, m, B, device=dev)
+        self.best_iter = torch.zeros(B, dtype=torch.int32, device=dev) if fixed_iters else None
         self.full_du_norm = torch.empty(B, device=dev)
         self.ws = torch.empty(T * B * ilqr_ws_floats(n, m), device=dev)
         self.ctrl = torch.zeros(2 * N.CTRL_INTS, dtype=torch.int32, device=dev)   # ping-pong control state
@@ -185,7 +191,8 @@ class MPCSolve:
         self.cost_sym = torch.zeros(B, dtype=torch.uint8, device=dev) if self.Cpk is not None else None
         self.state = N.MpcState(*[t.data_ptr() if t is not None else None for t in (
             self.Xs, self.Us, self.slot, self.best_cost, self.best_du, self.improved, self.cost, self.alpha,
-            self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter, self.Cpk, self.cost_sym)])
+            self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter, self.Cpk, self.cost_sym,
+            self.best_iter)])
 
     def begin(self, model_id, theta, x_init, u_init=None):
         """x = get_traj(u_init or 0) into slot 0; reset slots and the control block."""
@@ -211,6 +218,20 @@ class MPCSolve:
                N.ptr(c), bounds, float(decay), int(max_ls), int(iteration), float(best_cost_eps), float(eps),
                int(min(not_improved_lim, 2 ** 31 - 1)), self.state, N.stream(x_init.device))
         self.last_iteration = int(iteration)
+
+    def iterate_fixed(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, iteration, best_cost_eps):
+        """Iteration `iteration` of a fixed-count solve (one launch, no stop rule)."""
+        if not self.fixed_iters or not 0 <= iteration < self.fixed_iters:
+            raise ValueError("iterate_fixed: solve not built for a fixed count, or iteration out of range")
+        N.call("dilqr_mpc_iterate_fixed_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), N.ptr(C),
+               N.ptr(c), bounds, float(decay), int(max_ls), int(iteration), float(best_cost_eps), self.state,
+               N.stream(x_init.device))
+        self.last_iteration = int(iteration)
+
+    def finish_fixed(self, iterations):
+        """best_du of a fixed-count solve after `iterations` iterations."""
+        N.call("dilqr_mpc_finish_fixed_f32", self.T, self.m, self.B, int(iterations), self.state,
+               N.stream(self.Xs.device))
 
     def _ctrl_now(self):
         k = max(self.last_iteration, 0)
@@ -244,9 +265,20 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     B, n = x_init.shape
     m = C.shape[-1] - n
     x_init, C, c = _f32(x_init), _f32(C), _f32(c)
-    sv = MPCSolve(T, B, n, m, x_init.device)
+    # the stop rule (max full_du_norm < eps or n_not_improved > lim) cannot fire:
+    # one launch per iteration, best_du formed at the end (same values)
+    fixed = lqr_iter >= 1 and eps <= 0 and not_improved_lim >= lqr_iter
+    sv = MPCSolve(T, B, n, m, x_init.device, fixed_iters=lqr_iter if fixed else None)
     sv.begin(model_id, theta, x_init, u_init)
     bounds, keep = N.make_bounds(u_lower, u_upper)
+    if fixed:
+        for i in range(lqr_iter):
+            sv.iterate_fixed(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i,
+                             best_cost_eps)
+        sv.finish_fixed(lqr_iter)
+        del keep
+        x, u = sv.gather_best()
+        return x, u, sv.best_cost, sv.best_du, sv
     for i in range(lqr_iter):
         sv.iterate(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i,
                    best_cost_eps, eps, not_improved_lim)

@@ -245,6 +245,7 @@ typedef struct dilqr_mpc_state {
   int* improved; float* cost; float* alpha; float* du_sq; float* full_du_norm;
   float* ws; dilqr_mpc_ctrl* ctrl; unsigned* done_counter; float* Cpk;
   unsigned char* cost_sym;
+  int* best_iter;        /* [B], fixed-count solves only (NULL otherwise) */
 } dilqr_mpc_state;
 
 /* Start a solve: slot 0 = (get_traj(u), u) with u = u_init ([T,B,m], the
@@ -276,6 +277,23 @@ int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float*
                        dilqr_mpc_state st, void* stream);
 int dilqr_mpc_stop_rule_f32(int T, int m, int B, int iteration, dilqr_mpc_state st,
                             void* stream);
+
+/* Fixed-count solves: eps <= 0 and not_improved_lim >= the number of
+   iterations, so the stop rule (mpc_explicit.py:297-299) can never fire and
+   the solve runs all of them (the reference's loop does exactly that).  Each
+   iteration is ONE launch — the fused kernel with no stop-rule prologue — that
+   writes its du rows into plane `iteration` of du_sq (then [iters,T,m,B]) and
+   keeps in best_iter[B] the last iteration that took the best-iterate branch
+   (mpc_explicit.py:277-283).  dilqr_mpc_finish_fixed_f32 then forms best_du
+   from those planes (the quirk rows, lqr_step_explicit.py:245-247, bit for bit
+   the per-iteration rule's values) and sets ctrl[].iter; full_du_norm is not
+   maintained in this mode. */
+int dilqr_mpc_iterate_fixed_f32(int model, int T, int B, const float* theta, const float* x_init,
+                                const float* C, const float* c, dilqr_bounds bounds,
+                                float linesearch_decay, int max_linesearch_iter, int iteration,
+                                float best_cost_eps, dilqr_mpc_state st, void* stream);
+int dilqr_mpc_finish_fixed_f32(int T, int m, int B, int iterations, dilqr_mpc_state st,
+                               void* stream);
 
 /* Materialise each problem's best trajectory into x_out [T,B,n], u_out [T,B,m]. */
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out,

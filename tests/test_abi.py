@@ -86,3 +86,23 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in src and "from oracle" not in src, f
+
+
+@pytest.mark.parametrize("fixed", [None, 10])
+def test_mpc_solve_state_layout(fixed):
+    """The solve's device-state block (dilqr_mpc_state) is assembled with every
+    field the header declares, in order; best_iter is set only for fixed-count
+    solves, whose du_sq holds one [T,m,B] plane per iteration (CPU tensors
+    here: nothing is launched)."""
+    import torch
+    from dilqr import _native as N
+    from dilqr import ops
+    T, B, n, m = 7, 64, 5, 1
+    sv = ops.MPCSolve(T, B, n, m, torch.device("cpu"), fixed_iters=fixed)
+    names = [f for f, _ in N.MpcState._fields_]
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct dilqr_mpc_state \{(.*?)\} dilqr_mpc_state;", src, re.S).group(1)
+    assert names == re.findall(r"\*\s*(\w+)\s*;", body)
+    assert (sv.state.best_iter is not None) == bool(fixed)
+    assert sv.du_sq.shape == ((fixed or 1) * T, m, B)
+    assert all(getattr(sv.state, f) for f in names if f not in ("Cpk", "cost_sym", "best_iter"))

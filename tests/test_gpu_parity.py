@@ -356,6 +356,40 @@ def test_full_size_batch_independence():
     assert torch.isfinite(full[2]).all()
 
 
+@pytest.mark.parametrize("name", ["cart_unc", "cart_box10", "pend_box", "rocket_unc"])
+def test_fixed_count_solve_equals_stop_rule_path(golden, name):
+    """A solve whose stop rule cannot fire (eps <= 0, not_improved_lim >= the
+    iteration count) runs as a fixed-count solve: one launch per iteration and
+    best_du formed at the end (dilqr_mpc_iterate_fixed_f32 / finish).  Best
+    trajectories, best costs and best_du equal, bit for bit, those of the
+    per-iteration stop-rule path on the same problems."""
+    from dilqr import _native as N
+    from dilqr import ops
+    g = golden("mpc_f64")
+    mname, T, it, bounds, _eps, _nil, decay, mls = MPC_CASES[name]
+    dx = dilqr_models()[mname]()
+    x0 = gpu(g[f"{name}_x0"])
+    B, n, m = x0.shape[0], dx.n_state, dx.n_ctrl
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV).contiguous()
+    c = p.repeat(T, B, 1).to(DEV).contiguous()
+    theta = ops.theta_of(dx, x0)
+    lo, hi = bounds if bounds else (None, None)
+    bd, _keep = N.make_bounds(lo, hi)
+    a = ops.MPCSolve(T, B, n, m, x0.device)
+    a.begin(dx.model_id, theta, x0)
+    for i in range(it):
+        a.iterate(dx.model_id, theta, x0, C, c, bd, decay, mls, i, 1e-4, 0.0, 10 ** 9)
+    xa, ua = a.gather_best()
+    xb, ub, cost_b, du_b, sv = ops.mpc_solve(dx.model_id, theta, x0, C, c, T, u_lower=lo, u_upper=hi, lqr_iter=it,
+                                             eps=0.0, linesearch_decay=decay, max_linesearch_iter=mls,
+                                             not_improved_lim=10 ** 9)
+    assert sv.fixed_iters == it and sv.iterations == it
+    assert torch.equal(xa, xb) and torch.equal(ua, ub)
+    assert torch.equal(a.best_cost, cost_b) and torch.equal(a.best_du, du_b)
+    assert torch.isfinite(du_b).all()
+
+
 # ------------------------------------------------------------------ DiLQR implicit backward
 IMPLICIT = {"cart_unc": ("cartpole", None), "cart_box": ("cartpole", (-5.0, 5.0)),
             "pend_box": ("pendulum", (-2.0, 2.0)), "rock_unc": ("rocket", None),
