@@ -688,9 +688,10 @@ DEV S nonfinite_probe(const S (&tau)[D]) {
   return p;
 }
 
+// C tau alone (the sweep's c_back term when the stage cost itself is not
+// needed); the same expressions as quad_cost's, so the same bits
 template <int D, bool DIAG = false>
-DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D],
-                    float (&Ctau)[D]) {
+DEV void c_tau(const float (&C)[D][D], const float (&tau)[D], float (&Ctau)[D]) {
   float nf = 0.f;
   if constexpr (DIAG) nf = nonfinite_probe<D>(tau);
 #pragma unroll
@@ -704,6 +705,12 @@ DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&t
       Ctau[i] = s;
     }
   }
+}
+
+template <int D, bool DIAG = false>
+DEV float quad_cost(const float (&C)[D][D], const float (&c)[D], const float (&tau)[D],
+                    float (&Ctau)[D]) {
+  c_tau<D, DIAG>(C, tau, Ctau);
   float quad = 0.f, lin = 0.f;
 #pragma unroll
   for (int i = 0; i < D; ++i) {

@@ -433,13 +433,16 @@ __global__ void __launch_bounds__(kBlock) k_lqr_forward(int T, int B, const floa
                                                         const unsigned char* __restrict__ zI, float decay, int max_ls,
                                                         float* __restrict__ x_out, float* __restrict__ u_out,
                                                         float* __restrict__ cost_out, float* __restrict__ du_sq,
-                                                        float* __restrict__ alpha_out) {
+                                                        float* __restrict__ alpha_out,
+                                                        const float* __restrict__ old_cost_in) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   Dyn<n, m, Model> dyn;
   if constexpr (!std::is_same_v<Model, NoModel>) dyn.md.load(theta);
   dyn.F = F; dyn.f = f; dyn.B = B;
-  float old_cost = traj_cost<n, m>(T, B, b, C, c, x, u);        // lqr_step_explicit.py:171
+  // lqr_step_explicit.py:171, or the caller's value of the same cost (an MPC
+  // loop passes what its previous line search computed for this trajectory)
+  const float old_cost = old_cost_in ? old_cost_in[b] : traj_cost<n, m>(T, B, b, C, c, x, u);
   float alpha = 1.f, cost = 0.f;
   for (int ls = 0; ls < max_ls; ++ls) {
     cost = forward_pass<n, m, 0>(dyn, T, B, b, alpha, x_init, C, c, x, u, K, k, nullptr, bd, zI, x_out, u_out,
@@ -958,18 +961,23 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
 // records a later change of the cost proves necessary are written then, from
 // the registers holding that record), and a time-invariant diagonal cost is
 // handed to this iteration's line search in registers, so C is read once.
-template <class Model, int BM, int TL, bool ROLLOUT, class CostT>
+// PREV: the current trajectory's cost is prev_cost[b], the cost the previous
+// MPC iteration's line search computed for it (the accepted candidate), so the
+// sweep forms only C tau for c_back and not the stage costs again.
+template <class Model, int BM, int TL, bool ROLLOUT, class CostT, bool PREV = false>
 DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restrict__ x_init, const CostT& cs,
                      float* __restrict__ pack_out, unsigned char* __restrict__ sym_out, const float* __restrict__ x,
                      const float* __restrict__ u, const Bounds& bd, float decay, int max_ls,
                      const GainRecs& ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
                      float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
-                     float& cost_out, float& alpha_out, bool b_in_gains = false) {
+                     float& cost_out, float& alpha_out, bool b_in_gains = false,
+                     const float* __restrict__ prev_cost = nullptr) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
   constexpr int MODE = BM == DILQR_BOUNDS_NONE ? GAIN_UNC : GAIN_BOX;
   constexpr int GREC = m * n + m;                    // gain record: K, k (component-major)
   constexpr int PK = packed_cost_floats<d>();
   float old_cost = 0.f;                               // the current trajectory's cost, from the sweep
+  if constexpr (PREV) old_cost = prev_cost[b];        // ... or from the previous line search
   bool sym = true, diag = true, tinv = true;
   bool symsofar = true;                               // C_t' bitwise symmetric for all t' >= t (RiccatiState SYM)
   float pk_last[PK];                                  // step T-1's packed record (tinv test)
@@ -1015,7 +1023,9 @@ DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restric
           if (!tinv) SoaRec<PK>::store(pack_out, buf, T, t, B, b);
         }
       }
-      float obj = quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau, Ctau);
+      float obj = 0.f;
+      if constexpr (PREV) c_tau<d, CostT::kDiag>(cur.C, tau, Ctau);
+      else obj = quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau, Ctau);
 #pragma unroll
       for (int i = 0; i < d; ++i) cb[i] = Ctau[i] + cur.c[i];
       float Ft[n][d];
@@ -1052,7 +1062,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restric
         for (int j = 0; j < n; ++j) g[a * n + j] = Kt[a][j];
         g[m * n + a] = kt[a];
       }
-      old_cost += obj;          // summed over t = T-1..0 (the reference's torch sum has its own order)
+      if constexpr (!PREV) old_cost += obj;   // summed over t = T-1..0 (the reference's torch sum has its own order)
 #pragma unroll
       for (int i = 0; i < n; ++i) xn[i] = cur.x[i];
     };
@@ -1198,9 +1208,9 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
       if constexpr (packed_diag_ok<n + m>()) {
         CostDiagConst<n + m> cc;
         cc.init(S.Cpk, T, B, b);
-        win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd,
+        win = ilqr_problem<Model, BM, TRAJ_REC, true, CostDiagConst<n + m>, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd,
                                                       decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
-                                                      alpha, b_lds);
+                                                      alpha, b_lds, S.cost);
       } else {
         __builtin_unreachable();
       }
@@ -1211,23 +1221,23 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
 #else
     } else if (pk & kCostDiag) {           // set by iteration 0 only when packed_diag_ok
       if constexpr (packed_diag_ok<n + m>())
-        win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr,
+        win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m, true>, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr,
                                                       nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb,
-                                                      nullptr, S.du_sq, cost, alpha, b_lds);
+                                                      nullptr, S.du_sq, cost, alpha, b_lds, S.cost);
       else
         __builtin_unreachable();
     } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
-      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T},
+      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m, false, true>, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T},
                                                     nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr,
-                                                    xsb, nullptr, S.du_sq, cost, alpha, b_lds);
+                                                    xsb, nullptr, S.du_sq, cost, alpha, b_lds, S.cost);
     else if (pk & kCostSym)
-      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
+      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m>, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
                                                     xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
-                                                    S.du_sq, cost, alpha, b_lds);
+                                                    S.du_sq, cost, alpha, b_lds, S.cost);
     else
-      win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, nullptr, nullptr, xcur, nullptr, bd,
+      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostFull<n + m>, true>(T, B, b, md, x_init, full, nullptr, nullptr, xcur, nullptr, bd,
                                                     decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
-                                                    alpha, b_lds);
+                                                    alpha, b_lds, S.cost);
 #endif
   }
   DILQR_STAMP(3);
@@ -2177,7 +2187,7 @@ inline int launch_norm_rows(int TM, int B, int iteration, const MpcState& st, hi
 
 extern "C" {
 
-int dilqr_version(void) { return 3; }
+int dilqr_version(void) { return 4; }
 
 int dilqr_model_num_ctrl(int model) {
   switch (model) {
@@ -2307,7 +2317,7 @@ int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* th
                           const float* x_init, const float* C, const float* c, const float* x, const float* u,
                           const float* K, const float* k, dilqr_bounds bounds, const unsigned char* u_zero_I,
                           float linesearch_decay, int max_linesearch_iter, float* x_out, float* u_out, float* cost,
-                          float* du_sq, float* alpha, void* stream) {
+                          float* du_sq, float* alpha, const float* old_cost, void* stream) {
   if (T < 1 || B < 0 || max_linesearch_iter < 1) return DILQR_E_ARG;
   if (!x_init || !C || !c || !x || !u || !K || !k || !x_out || !u_out || !cost) return DILQR_E_ARG;
   const void* ps[] = {F, f, x_init, C, c, x, u, K, k, x_out, u_out};
@@ -2321,11 +2331,12 @@ int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* th
     if (n == N_ && m == M_) {                                                                                  \
       k_lqr_forward<N_, M_, NoModel><<<grid_for(B), kBlock, 0, S(stream)>>>(                                   \
           T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter,     \
-          x_out, u_out, cost, du_sq, alpha);                                                                   \
+          x_out, u_out, cost, du_sq, alpha, old_cost);                                                         \
       return launched();                                                                                       \
     }
     DILQR_FOR_EACH_SHAPE(X)
 #undef X
+    if (old_cost) return DILQR_E_MODE;                 // the 16-lane kernels form it themselves
 #define X(N_, M_)                                                                                             \
     if (n == N_ && m == M_) {                                                                                  \
       k_lqr_forward_group<N_, M_, GroupNoModel><<<grid_group(B), 64, 0, S(stream)>>>(                          \
@@ -2340,6 +2351,7 @@ int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* th
   if (!theta) return DILQR_E_ARG;
   if (model == DILQR_MODEL_ROCKET) {
     if (n != Rocket::N || m != Rocket::M) return DILQR_E_SHAPE;
+    if (old_cost) return DILQR_E_MODE;
     k_lqr_forward_group<Rocket::N, Rocket::M, Rocket><<<grid_group(B), 64, 0, S(stream)>>>(
         T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter, x_out,
         u_out, cost, du_sq, alpha);
@@ -2349,7 +2361,7 @@ int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* th
     if (n != MD::N || m != MD::M) return DILQR_E_SHAPE;
     k_lqr_forward<MD::N, MD::M, MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
         T, B, theta, F, f, x_init, C, c, x, u, K, k, bd, u_zero_I, linesearch_decay, max_linesearch_iter, x_out,
-        u_out, cost, du_sq, alpha);
+        u_out, cost, du_sq, alpha, old_cost);
   }));
   return launched();
 }

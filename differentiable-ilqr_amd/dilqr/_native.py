@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must be imported first: libdilqr.so then binds to t
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DILQR_LIB", os.path.join(_HERE, "libdilqr.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 MODEL_LINDX, MODEL_PENDULUM, MODEL_CARTPOLE, MODEL_ROCKET = 0, 1, 2, 3
 BOUNDS_NONE, BOUNDS_SCALAR, BOUNDS_TENSOR = 0, 1, 2
@@ -47,7 +47,7 @@ SIGNATURES = {
     "dilqr_lqr_backward_f32": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, Bounds, _vp, _i, _vp, _vp, _vp,
                                 _vp], _i),
     "dilqr_lqr_forward_f32": ([_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds,
-                               _vp, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+                               _vp, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_pnqp_f32": ([_i, _i, _vp, _vp, Bounds, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_quirk_norm_f32": ([_i, _i, _i, _vp, _vp, _vp], _i),
     "dilqr_ilqr_iterate_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _f, _i, _vp, _vp, _vp, _vp,

@@ -87,7 +87,7 @@ def lqr_forward(model_id, theta, x_init, C, c, x, u, K, k, F=None, f=None, u_low
     N.call("dilqr_lqr_forward_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f), N.ptr(x_init),
            N.ptr(C), N.ptr(c), N.ptr(x), N.ptr(u), N.ptr(K), N.ptr(k), bounds, N.ptr(zI),
            float(linesearch_decay), int(max_linesearch_iter), N.ptr(nx), N.ptr(nu), N.ptr(cost), N.ptr(du_sq),
-           N.ptr(alpha), N.stream(dev))
+           N.ptr(alpha), None, N.stream(dev))
     del keep
     return nx, nu, cost, du_sq, alpha
 
@@ -338,10 +338,13 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
             Fi, fi = linearize(model_id, theta, ws.xa, ws.ua)
         K, k, _ = lqr_backward(C, c, Fi, n, m, x=ws.xa, u=ws.ua, u_lower=u_lower, u_upper=u_upper)
         bounds, keep = N.make_bounds(u_lower, u_upper)
+        # from iteration 1 the old cost is the previous line search's value for
+        # the accepted candidate (ws.cost), as the fused MPC kernel takes it
+        prev = (N.ptr(ws.cost) if i > 0 and model_id in (N.MODEL_PENDULUM, N.MODEL_CARTPOLE) else None)
         N.call("dilqr_lqr_forward_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f),
                N.ptr(x_init), N.ptr(C), N.ptr(c), N.ptr(ws.xa), N.ptr(ws.ua), N.ptr(K), N.ptr(k), bounds, None,
                float(linesearch_decay), int(max_linesearch_iter), N.ptr(ws.xb), N.ptr(ws.ub), N.ptr(ws.cost),
-               N.ptr(ws.du_sq), N.ptr(ws.alpha), s)
+               N.ptr(ws.du_sq), N.ptr(ws.alpha), prev, s)
         N.call("dilqr_mpc_update_best_f32", n, m, T, B, int(i == 0), float(best_cost_eps), float(eps),
                int(min(not_improved_lim, 2 ** 31 - 1)), N.ptr(ws.xb), N.ptr(ws.ub), N.ptr(ws.cost),
                N.ptr(ws.du_sq), N.ptr(ws.fdn), N.ptr(ws.best_x), N.ptr(ws.best_u), N.ptr(ws.best_cost),

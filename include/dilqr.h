@@ -117,7 +117,11 @@ int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const flo
    lqr_step_explicit.py:166-263.  `model` gives the true dynamics (F/f for
    LINDX).  Outputs: new x/u, cost [B] (final pass), du_sq [T,m,B] =
    (u - new_u)^2 of the FIRST pass laid out [T,m,B] (input of
-   dilqr_quirk_norm_f32), alpha [B] = the alpha of the final pass. */
+   dilqr_quirk_norm_f32), alpha [B] = the alpha of the final pass.
+   old_cost [B] (nullable): the current trajectory's cost when the caller has
+   it (an MPC loop: its previous line search's value for the accepted
+   candidate), else formed from x, u (lqr_step_explicit.py:171); one lane per
+   problem models and LINDX d <= 8 only (DILQR_E_MODE otherwise). */
 int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* theta,
                           const float* F, const float* f, const float* x_init,
                           const float* C, const float* c, const float* x,
@@ -125,7 +129,7 @@ int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* th
                           dilqr_bounds bounds, const unsigned char* u_zero_I,
                           float linesearch_decay, int max_linesearch_iter,
                           float* x_out, float* u_out, float* cost, float* du_sq,
-                          float* alpha, void* stream);
+                          float* alpha, const float* old_cost, void* stream);
 
 /* The reference's batch-mixing norm (lqr_step_explicit.py:245-247):
    (u-new_u).transpose(1,2).contiguous().view(B,-1).norm(2,1), i.e. row r is
@@ -228,6 +232,9 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
    Cpk (nullable) + cost_sym [B] (uint8): the solve's packed copy of a
    symmetric cost, T*B*dilqr_mpc_packed_cost_floats(n,m) floats (diag of C_t,b,
    then c_t,b, then the strict upper triangle row-major; component-major).
+   From iteration 1 on, the fused kernel takes the current trajectory's cost
+   (the line search's old cost) from cost[B], which the previous iteration's
+   line search wrote for the accepted candidate, instead of summing it again.
    Iteration 0 (first != 0) reads C, c and writes the copy and, per problem,
    flags: bit 0 all its C_t bitwise symmetric, bit 1 all off-diagonals +0.0 too.
    Later iterations of flagged problems read the copy: 27 instead of 42 floats
