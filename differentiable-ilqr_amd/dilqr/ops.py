@@ -267,7 +267,9 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     x_init, C, c = _f32(x_init), _f32(C), _f32(c)
     # the stop rule (max full_du_norm < eps or n_not_improved > lim) cannot fire:
     # one launch per iteration, best_du formed at the end (same values)
-    fixed = lqr_iter >= 1 and eps <= 0 and not_improved_lim >= lqr_iter
+    # (the per-iteration du planes are kept: up to 2 GiB of them)
+    fixed = (lqr_iter >= 1 and eps <= 0 and not_improved_lim >= lqr_iter
+             and 4 * lqr_iter * T * m * B <= 2 ** 31)
     sv = MPCSolve(T, B, n, m, x_init.device, fixed_iters=lqr_iter if fixed else None)
     sv.begin(model_id, theta, x_init, u_init)
     bounds, keep = N.make_bounds(u_lower, u_upper)
