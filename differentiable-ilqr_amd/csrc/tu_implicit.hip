@@ -1,0 +1,346 @@
+// tu_implicit.hip — the DiLQR implicit backward for the one-problem-per-lane
+// models (pendulum, cartpole); rocket's 16-lane kernel is in tu_implicit_rocket.hip.
+#include "dilqr_common.h"
+#include "dilqr_launch.h"
+
+namespace dilqr {
+
+// ============================================================ DiLQR implicit backward
+// lqr_step_explicit.py:653-712 + fix_point_equ 458-598, by the algebra of
+// oracle/adjoint.py implicit_backward_fast (validated against the literal
+// restatement to 1e-14 in fp64): the reference's (T d)^2 system A^T w = g is one
+// extra LQR solve with cost C_t + M_t^T, M_t = sum_i lam_{t+1,i} d D_t[i] / d tau
+// (the Lagrangian Hessian of the dynamics), after which dC, dc, dtheta are the
+// KKT gradients of the adjoint solve with r = w, whose trajectory is that same
+// solve's y.  Per problem (one lane), four passes over T:
+//   A (t up)   : gradx_t (grad_input's closed-loop d x_t / d theta, with the
+//                reference's reversed-K and x_grad_xtm1 quirks) -> ws
+//   B (t down) : primal costates lam_t -> ws; M_t; Riccati step with C_t + M_t^T,
+//                c_back = -g_t, active set masked (u_zero_I engine) -> ws
+//   C (t up)   : rollout y (no line search) -> ws
+//   D (t down) : w_t = g_t - M_t^T y_t, dlam; dC_t, dc_t out; dtheta accumulated.
+template <class Model> struct ImplicitWs {
+  static constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m;
+  static constexpr int GX = 0, LAM = n * p, KG = LAM + n, Y = KG + m * n + m;
+  static constexpr int REC = ((Y + d) + 3) / 4 * 4;
+};
+
+template <class Model>
+__global__ void __launch_bounds__(kBlock) k_implicit_backward(
+    int T, int B, const float* __restrict__ theta, const float* __restrict__ C, const float* __restrict__ c,
+    const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ K,
+    const float* __restrict__ dl_dx, const float* __restrict__ dl_du, Bounds bd, float* __restrict__ ws,
+    float* __restrict__ dC, float* __restrict__ dc, float* __restrict__ dtheta) {
+  using D2 = typename D2Of<Model>::type;
+  using W = ImplicitWs<Model>;
+  constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m, R = W::REC;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Model md; md.load(theta);
+  auto rec = [&](int t) { return ws + ((size_t)t * B + b) * R; };
+  auto active = [&](size_t tb, int a, float ua) -> bool {
+    if (bd.mode == DILQR_BOUNDS_NONE) return false;
+    return fabsf(ua - bound_lo(bd, tb * m + a)) <= 1e-8f || fabsf(ua - bound_hi(bd, tb * m + a)) <= 1e-8f;
+  };
+  // ---------------- A: gradx_t, t = 0..T-1  (cartpole.py:755-769)
+  {
+    float gx[n][p];
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+#pragma unroll
+      for (int k = 0; k < p; ++k) gx[i][k] = 0.f;
+    st2(rec(0) + W::GX, gx);
+    for (int t = 1; t < T; ++t) {
+      size_t tb = (size_t)t * B + b;
+      float xt[n], ut[m], D[n][d], ft[n][p], Kq[m][n];
+      ld(xt, x + tb * n); ld(ut, u + tb * m);
+      md.jacobian(xt, ut, D);
+      D2::f_theta(theta, xt, ut, ft);
+      ld2(Kq, K + ((size_t)(T - t) * B + b) * m * n);     // K[t-1] of the reversed stack = K_{T-t}
+      float A[n][n];
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+#pragma unroll
+        for (int l = 0; l < n; ++l) {
+          float s = D[i][l];
+          if (D2Of<Model>::XX00_ZERO && i == 0 && l == 0) s = 0.f;
+#pragma unroll
+          for (int a = 0; a < m; ++a) s += D[i][n + a] * Kq[a][l];
+          A[i][l] = s;
+        }
+      float ng[n][p];
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+#pragma unroll
+        for (int k = 0; k < p; ++k) {
+          float s = 0.f;
+#pragma unroll
+          for (int l = 0; l < n; ++l) s += A[i][l] * gx[l][k];
+          ng[i][k] = ft[i][k] + s;
+        }
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+#pragma unroll
+        for (int k = 0; k < p; ++k) gx[i][k] = ng[i][k];
+      st2(rec(t) + W::GX, gx);
+    }
+  }
+  // ---------------- B: costates, M_t, Riccati of the C + M^T problem
+  {
+    RiccatiState<n, m> rs;
+    rs.init();
+    float lam[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) lam[i] = 0.f;
+    for (int t = T - 1; t >= 0; --t) {
+      size_t tb = (size_t)t * B + b;
+      float Ct[d][d], ct[d], xt[n], ut[m], gxx[n], gu[m];
+      ld2(Ct, C + tb * d * d); ld(ct, c + tb * d); ld(xt, x + tb * n); ld(ut, u + tb * m);
+      ld(gxx, dl_dx + tb * n); ld(gu, dl_du + tb * m);
+      float D[n][d];
+      float Mt[d][d];
+      if (t < T - 1) {
+        md.jacobian(xt, ut, D);
+        D2::lag_hess(theta, xt, ut, lam, Mt);             // lam = lam_{t+1}
+      } else {
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int j = 0; j < d; ++j) D[i][j] = 0.f;
+#pragma unroll
+        for (int i = 0; i < d; ++i)
+#pragma unroll
+          for (int j = 0; j < d; ++j) Mt[i][j] = 0.f;
+      }
+      float Cp[d][d], cb[d];
+#pragma unroll
+      for (int i = 0; i < d; ++i)
+#pragma unroll
+        for (int j = 0; j < d; ++j) Cp[i][j] = Ct[i][j] + Mt[j][i];
+#pragma unroll
+      for (int i = 0; i < n; ++i) cb[i] = -gxx[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) cb[n + a] = -gu[a];
+      float zI[m], lb[m], ub[m];
+#pragma unroll
+      for (int a = 0; a < m; ++a) { zI[a] = active(tb, a, ut[a]) ? 1.f : 0.f; lb[a] = ub[a] = 0.f; }
+      float Kt[m][n], kt[m];
+      if (bd.mode != DILQR_BOUNDS_NONE) rs.template step<GAIN_ZERO_I>(Cp, cb, D, zI, lb, ub, Kt, kt);
+      else rs.template step<GAIN_UNC>(Cp, cb, D, zI, lb, ub, Kt, kt);
+      float* r = rec(t);
+      st2(r + W::KG, Kt);
+#pragma unroll
+      for (int a = 0; a < m; ++a) r[W::KG + m * n + a] = kt[a];
+      // lam_t = Cxx x + Cxu u + c_x + F_x^T lam_{t+1}   (lqr_step_explicit.py:305-319)
+      float nl[n];
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += Ct[i][j] * xt[j];
+#pragma unroll
+        for (int a = 0; a < m; ++a) s2 += Ct[i][n + a] * ut[a];
+        float s3 = 0.f;
+#pragma unroll
+        for (int l = 0; l < n; ++l) s3 += D[l][i] * lam[l];
+        nl[i] = ((s + s2) + ct[i]) + s3;
+      }
+#pragma unroll
+      for (int i = 0; i < n; ++i) { lam[i] = nl[i]; r[W::LAM + i] = nl[i]; }
+    }
+  }
+  // ---------------- C: rollout y of the modified problem (linear, alpha = 1)
+  {
+    float yx[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) yx[i] = 0.f;
+    for (int t = 0; t < T; ++t) {
+      size_t tb = (size_t)t * B + b;
+      float* r = rec(t);
+      float Kt[m][n], kt[m], ut[m];
+      ld2(Kt, r + W::KG);
+#pragma unroll
+      for (int a = 0; a < m; ++a) kt[a] = r[W::KG + m * n + a];
+      ld(ut, u + tb * m);
+      float y[d];
+#pragma unroll
+      for (int i = 0; i < n; ++i) y[i] = yx[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += Kt[a][j] * yx[j];
+        y[n + a] = active(tb, a, ut[a]) ? 0.f : (s + 0.f) + kt[a];
+      }
+#pragma unroll
+      for (int i = 0; i < d; ++i) r[W::Y + i] = y[i];
+      if (t < T - 1) {
+        float xt[n], D[n][d];
+        ld(xt, x + tb * n);
+        md.jacobian(xt, ut, D);
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < d; ++j) s += D[i][j] * y[j];
+          yx[i] = s;
+        }
+      }
+    }
+  }
+  // ---------------- D: w, dlam, dC, dc, dtheta
+  {
+    float dlam[n], gx1[n][p], dth[p];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      dlam[i] = 0.f;
+#pragma unroll
+      for (int k = 0; k < p; ++k) gx1[i][k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < p; ++k) dth[k] = 0.f;
+    for (int t = T - 1; t >= 0; --t) {
+      size_t tb = (size_t)t * B + b;
+      float* r = rec(t);
+      float Ct[d][d], xt[n], ut[m], gxx[n], gu[m], y[d], gx[n][p];
+      ld2(Ct, C + tb * d * d); ld(xt, x + tb * n); ld(ut, u + tb * m);
+      ld(gxx, dl_dx + tb * n); ld(gu, dl_du + tb * m);
+#pragma unroll
+      for (int i = 0; i < d; ++i) y[i] = r[W::Y + i];
+      ld2(gx, r + W::GX);
+      float tau[d];
+#pragma unroll
+      for (int i = 0; i < n; ++i) tau[i] = xt[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+      // dC_t = -0.5 (y tau^T + tau y^T), dc_t = -y   (lqr_step_explicit.py:296-303)
+      float dCt[d][d], dct[d];
+#pragma unroll
+      for (int i = 0; i < d; ++i) {
+#pragma unroll
+        for (int j = 0; j < d; ++j) dCt[i][j] = -0.5f * (y[i] * tau[j] + tau[i] * y[j]);
+        dct[i] = -y[i];
+      }
+      st2(dC + tb * d * d, dCt);
+      st(dc + tb * d, dct);
+      float wx[n];
+      float D[n][d];
+      if (t < T - 1) {
+        float lam1[n], Mt[d][d], Mp[d][p], Kq[m][n];
+#pragma unroll
+        for (int i = 0; i < n; ++i) lam1[i] = rec(t + 1)[W::LAM + i];
+        md.jacobian(xt, ut, D);
+        D2::lag_hess(theta, xt, ut, lam1, Mt);
+        D2::lag_dparam(theta, xt, ut, lam1, Mp);
+        ld2(Kq, K + ((size_t)(T - 1 - t) * B + b) * m * n);   // K[t] of the reversed stack
+        // w_t = g_t - M_t^T y_t
+#pragma unroll
+        for (int k = 0; k < n; ++k) {
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < d; ++j) s += Mt[j][k] * y[j];
+          wx[k] = gxx[k] - s;
+        }
+        // dtheta_t = -(y^T Mp) - (y^T (M_x + M_u Kq)) gradx_t - dlam_{t+1}^T gradx_{t+1}
+        //            + dlam_{t+1}^T (D_x + D_u Kq) gradx_t
+        float hx[n], hp[p];
+#pragma unroll
+        for (int k = 0; k < p; ++k) {
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < d; ++j) s += y[j] * Mp[j][k];
+          hp[k] = s;
+        }
+#pragma unroll
+        for (int l = 0; l < n; ++l) {
+          float s = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int j = 0; j < d; ++j) {
+            float ml = Mt[j][l];
+#pragma unroll
+            for (int a = 0; a < m; ++a) ml += Mt[j][n + a] * Kq[a][l];
+            s += y[j] * ml;
+          }
+#pragma unroll
+          for (int i = 0; i < n; ++i) {
+            float dl = D[i][l];
+#pragma unroll
+            for (int a = 0; a < m; ++a) dl += D[i][n + a] * Kq[a][l];
+            s2 += dlam[i] * dl;
+          }
+          hx[l] = s2 - s;
+        }
+#pragma unroll
+        for (int k = 0; k < p; ++k) {
+          float s = -hp[k];
+#pragma unroll
+          for (int l = 0; l < n; ++l) s += hx[l] * gx[l][k] - dlam[l] * gx1[l][k];
+          dth[k] += s;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < n; ++k) wx[k] = gxx[k];
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int j = 0; j < d; ++j) D[i][j] = 0.f;
+      }
+      // dlam_t = Cxx y_x + Cxu y_u - w_x + F_x^T dlam_{t+1}   (lqr_step_explicit.py:321-335)
+      float nd[n];
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        float s = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) s += Ct[i][j] * y[j];
+#pragma unroll
+        for (int a = 0; a < m; ++a) s2 += Ct[i][n + a] * y[n + a];
+#pragma unroll
+        for (int l = 0; l < n; ++l) s3 += D[l][i] * dlam[l];
+        nd[i] = ((s + s2) - wx[i]) + s3;
+      }
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        dlam[i] = nd[i];
+#pragma unroll
+        for (int k = 0; k < p; ++k) gx1[i][k] = gx[i][k];
+      }
+    }
+    st(dtheta + (size_t)b * p, dth);
+  }
+}
+
+}  // namespace dilqr
+
+using namespace dilqr;
+
+extern "C" {
+
+int dilqr_implicit_ws_floats(int model) {
+  switch (model) {
+    case DILQR_MODEL_PENDULUM: return ImplicitWs<Pendulum>::REC;
+    case DILQR_MODEL_CARTPOLE: return ImplicitWs<Cartpole>::REC;
+    case DILQR_MODEL_ROCKET: return implicit_rocket_ws_floats();
+    default: return -1;
+  }
+}
+
+int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta, const float* C, const float* c,
+                                const float* x, const float* u, const float* K, const float* dl_dx,
+                                const float* dl_du, dilqr_bounds bounds, float* ws, float* dC, float* dc,
+                                float* dtheta, void* stream) {
+  if (T < 1 || B < 0) return DILQR_E_ARG;
+  if (!theta || !C || !c || !x || !u || !K || !dl_dx || !dl_du || !ws || !dC || !dc || !dtheta) return DILQR_E_ARG;
+  const void* ps[] = {C, c, x, u, K, dl_dx, dl_du, ws, dC, dc, dtheta};
+  for (const void* q : ps) if (!al16(q)) return DILQR_E_ARG;
+  if (bad_bounds(bounds)) return DILQR_E_ARG;
+  if (B == 0) return 0;
+  Bounds bd = mkb(bounds);
+  if (model == DILQR_MODEL_ROCKET)
+    return launch_implicit_rocket(ImplicitArgs{T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta,
+                                               S(stream)});
+  MODEL_SWITCH_TPP(model, (k_implicit_backward<MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
+                          T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta)));
+  return launched();
+}
+
+}  // extern "C"

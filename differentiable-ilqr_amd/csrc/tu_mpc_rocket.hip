@@ -1,0 +1,99 @@
+// tu_mpc_rocket.hip — the fused iteration for the 16-lanes-per-problem model
+// (env_dx/rocket.py, n=13 m=3): standalone and device-resident MPC kernels.
+#include "dilqr_fused.h"
+
+namespace dilqr {
+
+// the same two kernels for the 16-lanes-per-problem models (dilqr_group.h)
+template <class Model, int MODE>
+__global__ void __launch_bounds__(64) k_ilqr_iterate_group(int T, int B, const float* __restrict__ theta,
+                                                           const float* __restrict__ x_init,
+                                                           const float* __restrict__ C, const float* __restrict__ c,
+                                                           const float* __restrict__ x, const float* __restrict__ u,
+                                                           Bounds bd, float decay, int max_ls, float* __restrict__ ws,
+                                                           float* __restrict__ x_out, float* __restrict__ u_out,
+                                                           float* __restrict__ cost_out, float* __restrict__ du_sq,
+                                                           float* __restrict__ alpha_out,
+                                                           const dilqr_mpc_ctrl* __restrict__ ctrl) {
+  __shared__ GroupLds<Model::N, Model::M> Ls[kGPW];
+  if (ctrl && ctrl->stopped) return;
+  const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
+  const int b0 = blockIdx.x * kGPW + gp;
+  const bool valid = b0 < B;
+  const int b = valid ? b0 : B - 1;          // idle groups shadow problem B-1 (same wave), writing nothing
+  Model md; md.load(theta);
+  float cost, alpha;
+  int win;
+  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, x, u, bd, decay, max_ls, ws, x_out,
+                                  u_out, nullptr, nullptr, du_sq, cost, alpha, win);
+  if (valid && r == 0) {
+    cost_out[b] = cost;
+    alpha_out[b] = alpha;
+  }
+}
+
+template <class Model, int MODE>
+__global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_mpc_iterate_group(int T, int B, const float* __restrict__ theta,
+                                                          const float* __restrict__ x_init,
+                                                          const float* __restrict__ C, const float* __restrict__ c,
+                                                          Bounds bd, float decay, int max_ls, int iteration,
+                                                          float best_cost_eps, float eps, int not_improved_lim, int G,
+                                                          MpcState S) {
+  constexpr int n = Model::N, m = Model::M;
+  __shared__ GroupLds<n, m> Ls[kGPW];
+  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
+  const int first = iteration == 0;
+  const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
+  const int b0 = blockIdx.x * kGPW + gp;
+  const bool valid = b0 < B;
+  const int b = valid ? b0 : B - 1;
+  Model md; md.load(theta);
+  const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
+  const int cur = S.slot[b], best = S.slot[B + b];
+  int sa, sb;
+  free_slots(cur, best, sa, sb);
+  float cost, alpha;
+  int win;
+  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, S.Xs + cur * TBn, S.Us + cur * TBm,
+                                  bd, decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
+                                  S.Us + sb * TBm, S.du_sq, cost, alpha, win);
+  const int nw = win ? sb : sa;
+  if (valid && r == 0) {
+    S.cost[b] = cost;
+    S.alpha[b] = alpha;
+    const bool better = !first && (cost <= S.best_cost[b] + best_cost_eps);   // mpc_explicit.py:278
+    if (first || better) {
+      S.best_cost[b] = cost;
+      S.slot[B + b] = (unsigned char)nw;
+    }
+    S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
+    if (S.best_iter && (first || better)) S.best_iter[b] = iteration;     // fixed-count solves
+    S.slot[b] = (unsigned char)nw;
+  }
+}
+
+int launch_mpc_step_rocket(const MpcStepArgs& a) {
+  if (a.bd.mode != DILQR_BOUNDS_NONE)
+    k_mpc_iterate_group<Rocket, GAIN_BOX><<<grid_group(a.B), 64, 0, a.stream>>>(
+        a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.eps, a.lim,
+        a.G, a.st);
+  else
+    k_mpc_iterate_group<Rocket, GAIN_UNC><<<grid_group(a.B), 64, 0, a.stream>>>(
+        a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.eps, a.lim,
+        a.G, a.st);
+  return launched();
+}
+
+int launch_ilqr_iterate_rocket(const IlqrIterArgs& a) {
+  if (a.bd.mode != DILQR_BOUNDS_NONE)
+    k_ilqr_iterate_group<Rocket, GAIN_BOX><<<grid_group(a.B), 64, 0, a.stream>>>(
+        a.T, a.B, a.theta, a.x_init, a.C, a.c, a.x, a.u, a.bd, a.decay, a.max_ls, a.ws, a.x_out, a.u_out, a.cost,
+        a.du_sq, a.alpha, a.ctrl);
+  else
+    k_ilqr_iterate_group<Rocket, GAIN_UNC><<<grid_group(a.B), 64, 0, a.stream>>>(
+        a.T, a.B, a.theta, a.x_init, a.C, a.c, a.x, a.u, a.bd, a.decay, a.max_ls, a.ws, a.x_out, a.u_out, a.cost,
+        a.du_sq, a.alpha, a.ctrl);
+  return launched();
+}
+
+}  // namespace dilqr

@@ -6,13 +6,16 @@ stream as a void*.  There is NO fallback: if the library is missing, or a tensor
 is not on the GPU, every call raises.
 """
 import ctypes
+import glob
+import hashlib
 import os
 
 import torch  # noqa: F401  (must be imported first: libdilqr.so then binds to torch's HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DILQR_LIB", os.path.join(_HERE, "libdilqr.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
+_PKG = os.path.dirname(_HERE)          # differentiable-ilqr_amd/ (the Makefile's directory)
 
 MODEL_LINDX, MODEL_PENDULUM, MODEL_CARTPOLE, MODEL_ROCKET = 0, 1, 2, 3
 BOUNDS_NONE, BOUNDS_SCALAR, BOUNDS_TENSOR = 0, 1, 2
@@ -37,6 +40,7 @@ class MpcState(ctypes.Structure):
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 SIGNATURES = {
     "dilqr_version": ([], _i),
+    "dilqr_build_id": ([], ctypes.c_char_p),
     "dilqr_model_num_params": ([_i], _i),
     "dilqr_model_num_ctrl": ([_i], _i),
     "dilqr_dynamics_f32": ([_i, _i, _vp, _vp, _vp, _vp, _vp], _i),
@@ -72,6 +76,22 @@ SIGNATURES = {
 _lib = None
 
 
+def tree_build_id():
+    """The Makefile's BUILD_ID recomputed from the sources in this tree: sha256
+    of csrc/*.hip, csrc/*.h and ../include/dilqr.h concatenated in byte-sorted
+    path order, first 16 hex digits.  None when the sources are not present."""
+    names = [os.path.relpath(f, _PKG) for f in glob.glob(os.path.join(_PKG, "csrc", "*.hip"))
+             + glob.glob(os.path.join(_PKG, "csrc", "*.h"))]
+    names.append(os.path.join("..", "include", "dilqr.h"))
+    if not all(os.path.exists(os.path.join(_PKG, n)) for n in names) or len(names) < 2:
+        return None
+    h = hashlib.sha256()
+    for n in sorted(names):
+        with open(os.path.join(_PKG, n), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def lib():
     """Load libdilqr.so once; raise if it is missing (no CPU fallback)."""
     global _lib
@@ -89,6 +109,12 @@ def lib():
         v = handle.dilqr_version()
         if v != ABI_VERSION:
             raise RuntimeError(f"dilqr: library ABI {v} != expected {ABI_VERSION}")
+        built = handle.dilqr_build_id().decode()
+        tree = tree_build_id()
+        if tree is not None and built != tree and not os.environ.get("DILQR_SKIP_BUILD_ID"):
+            raise RuntimeError(
+                f"dilqr: {LIB_PATH} was built from other sources (build id {built}, tree {tree}); "
+                "rebuild it with `make -C differentiable-ilqr_amd`")
         _lib = handle
     return _lib
 

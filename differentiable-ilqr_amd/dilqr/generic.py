@@ -212,7 +212,7 @@ def approximate_cost(x, u, cost, diff):
 
 # ---------------------------------------------------------------- one LQR step (forward)
 def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u_lower, u_upper, delta_u,
-                     decay, max_ls):
+                     decay, max_ls, u_zero_I=None):
     """LQRStepFn.forward of the DiLQR step (lqr_step_explicit.py:625-650): the
     HIP Riccati sweep in delta space (c_back = C tau + c fused), then the line
     search of lqr_forward (166-263) with the true dynamics/cost.  Returns
@@ -220,18 +220,20 @@ def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u
     B = x.shape[1]
     lo = u_lower if (u_lower is None or isinstance(u_lower, float)) else u_lower.detach().contiguous()
     hi = u_upper if (u_upper is None or isinstance(u_upper, float)) else u_upper.detach().contiguous()
-    rlo, rhi = lo, hi
-    if delta_u is not None and lo is not None:
-        # lqr_step_explicit.py:132-135: the sweep's box is also clipped to
-        # +-delta_u around u_t; as absolute bounds for the kernel (which forms
-        # bound - u_t) that is max(lower, u_t - delta_u) / min(upper, u_t + delta_u)
-        ud = u.detach()
-        lo_t = lo if isinstance(lo, torch.Tensor) else torch.full_like(ud, lo)
-        hi_t = hi if isinstance(hi, torch.Tensor) else torch.full_like(ud, hi)
-        rlo = torch.where(lo_t - ud < -delta_u, ud - delta_u, lo_t).contiguous()
-        rhi = torch.where(hi_t - ud > delta_u, ud + delta_u, hi_t).contiguous()
-    K, k, _ = ops.lqr_backward(C.detach().contiguous(), c.detach().contiguous(), F.detach().contiguous(), n, m,
-                               x=x.detach().contiguous(), u=u.detach().contiguous(), u_lower=rlo, u_upper=rhi)
+    if delta_u is not None and lo is None:
+        raise NotImplementedError("dilqr: delta_u without u_lower is unimplemented in the reference too "
+                                  "(lqr_step_explicit.py:197)")
+    zI = None if u_zero_I is None else u_zero_I.detach().bool()
+    xd, ud = x.detach().contiguous(), u.detach().contiguous()
+    Cd, cd, Fd = C.detach().contiguous(), c.detach().contiguous(), F.detach().contiguous()
+    if delta_u is not None:
+        # lqr_step_explicit.py:132-135: the sweep's relative box clipped to
+        # +-delta_u (exact values), c_back formed here
+        rlo, rhi = ops.delta_u_sweep_bounds(lo, hi, ud, delta_u)
+        K, k, _ = ops.lqr_backward(Cd, ops.c_back(Cd, cd, xd, ud), Fd, n, m, u_lower=rlo, u_upper=rhi)
+    else:
+        K, k, _ = ops.lqr_backward(Cd, cd, Fd, n, m, x=xd, u=ud, u_lower=lo, u_upper=hi,
+                                   u_zero_I=zI if lo is None else None)
     old_cost = traj_cost(T, x, u, true_cost)
     alphas = torch.ones(B, device=x.device)
     cur_cost, full_du_norm = None, None
@@ -241,6 +243,8 @@ def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u
             new_u, new_x, dxs, objs = [], [x_init.detach()], torch.zeros_like(x_init), []
             for t in range(T):
                 nu = bmv(K[t], dxs) + u[t] + alphas.unsqueeze(1) * k[t]
+                if zI is not None:                              # lqr_step_explicit.py:199-200
+                    nu = torch.where(zI[t], torch.zeros_like(nu), nu)
                 if lo is not None:
                     lb = lo if isinstance(lo, float) else lo[t]
                     ub = hi if isinstance(hi, float) else hi[t]
@@ -320,11 +324,13 @@ def solve_subproblem(mpc, x_init, C, c, F, f, cost, dynamics, x, u):
     T, n, m = mpc.T, mpc.n_state, mpc.n_ctrl
     if mpc.slew_rate_penalty is None or isinstance(cost, torch.nn.Module):
         return lqr_step_forward(T, n, m, x_init, C, c, F, x, u, cost, dynamics, mpc.u_lower, mpc.u_upper,
-                                mpc.delta_u, mpc.linesearch_decay, mpc.max_linesearch_iter)
+                                mpc.delta_u, mpc.linesearch_decay, mpc.max_linesearch_iter,
+                                getattr(mpc, "u_zero_I", None))
     _x_init, _C, _c, _F, _f, _dyn, _cost, _x = slew_augment(mpc, x_init, C, c, F, f, cost, dynamics, x, u)
     true_dyn = _dyn if _dyn is not None else LinDx(_F, _f)
     nx, nu, costs, fdn = lqr_step_forward(T, n + m, m, _x_init, _C, _c, _F, _x, u, _cost, true_dyn, mpc.u_lower,
-                                          mpc.u_upper, mpc.delta_u, mpc.linesearch_decay, mpc.max_linesearch_iter)
+                                          mpc.u_upper, mpc.delta_u, mpc.linesearch_decay, mpc.max_linesearch_iter,
+                                          getattr(mpc, "u_zero_I", None))
     return nx[:, :, m:], nu, costs, fdn
 
 
@@ -409,10 +415,20 @@ def final_step(mpc, x_init, cost, dx, x, u, classic):
     if getattr(dx, "model_id", None) not in (N.MODEL_CARTPOLE, N.MODEL_PENDULUM, N.MODEL_ROCKET):
         # the DiLQR implicit backward needs an env_dx model's second derivatives
         # (the reference reads dx.params and dx.grad_input and raises without
-        # them); the solution is returned without a graph
+        # them, mpc_explicit.py:325, lqr_step_explicit.py:703): a caller whose
+        # inputs carry gradients gets the same refusal, never a silently
+        # detached solution; without gradients there is nothing to attach
+        wants = [t for t in (x_init, C, c, F, f) if isinstance(t, torch.Tensor) and t.requires_grad]
+        if wants:
+            raise NotImplementedError(
+                "dilqr: mpc_explicit.MPC differentiates through the DiLQR implicit backward, which needs an "
+                "env_dx model (cartpole, pendulum, rocket); use mpc.MPC (classic adjoint) for LinDx or "
+                "generic dynamics, or solve under torch.no_grad()")
         return x.detach(), u.detach()
     th = dx.params if isinstance(dx.params, torch.Tensor) else torch.tensor(dx.params)
-    step = ExplicitStep(n, m, T, u_lower=mpc.u_lower, u_upper=mpc.u_upper, true_cost=QuadCost(C, c),
-                        true_dynamics=dx, current_x=x.detach(), current_u=u.detach(), back_eps=mpc.back_eps,
-                        no_op_forward=True)
+    # the no-op step's sweep (its gains feed the implicit backward) sees the
+    # same mask / trust region as the loop's (mpc_explicit.py:369, 452)
+    step = ExplicitStep(n, m, T, u_lower=mpc.u_lower, u_upper=mpc.u_upper, u_zero_I=getattr(mpc, "u_zero_I", None),
+                        delta_u=mpc.delta_u, true_cost=QuadCost(C, c), true_dynamics=dx, current_x=x.detach(),
+                        current_u=u.detach(), back_eps=mpc.back_eps, no_op_forward=True)
     return step(x_init, C, c, F, f, th)

@@ -31,11 +31,23 @@ def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta
             linesearch_decay=0.2, max_linesearch_iter=10, true_cost=None, true_dynamics=None,
             delta_space=True, current_x=None, current_u=None, verbose=0, back_eps=1e-3,
             no_op_forward=False, theta=None):
-    if delta_u is not None:
-        raise NotImplementedError("dilqr: delta_u is not on the HIP path")
     if not delta_space:
         raise NotImplementedError("dilqr: delta_space=False is unimplemented in the reference too (639)")
+    if delta_u is not None and u_lower is None:
+        raise NotImplementedError("dilqr: delta_u without u_lower is unimplemented in the reference too (197)")
     lo, hi = _bounds_arg(u_lower), _bounds_arg(u_upper)
+    zI = None if u_zero_I is None else u_zero_I.detach()
+
+    def sweep(C, c, F, x, u, want_nqp=False):
+        """lqr_backward (54-162): c_back fused into the kernel; with delta_u the
+        box is relative and clipped to +-delta_u (132-135), c_back formed here;
+        the u_zero_I mask applies only without bounds (the pnqp branch ignores it)."""
+        if delta_u is not None:
+            rlo, rhi = ops.delta_u_sweep_bounds(lo, hi, u, delta_u)
+            return ops.lqr_backward(C, ops.c_back(C.detach(), c.detach(), x, u), F, n_state, n_ctrl,
+                                    u_lower=rlo, u_upper=rhi, want_nqp=want_nqp)
+        return ops.lqr_backward(C, c, F, n_state, n_ctrl, x=x, u=u, u_lower=lo, u_upper=hi,
+                                u_zero_I=zI if lo is None else None, want_nqp=want_nqp)
 
     class LQRStepFn(Function):
         @staticmethod
@@ -44,15 +56,13 @@ def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta
             x, u = current_x.detach(), current_u.detach()
             m_id = ops.model_id_of(true_dynamics)
             if no_op_forward:
-                K, _, _ = ops.lqr_backward(C, c, F, n_state, n_ctrl, x=x, u=u, u_lower=lo, u_upper=hi,
-                                           u_zero_I=u_zero_I)
+                K, _, _ = sweep(C, c, F, x, u)
                 ctx.save_for_backward(x_init, C, c, F, f, x, u, theta, K)
                 ctx.model = true_dynamics
                 return x.clone(), u.clone()
             if not isinstance(true_cost, QuadCost):
                 raise NotImplementedError("dilqr: true_cost must be a QuadCost on the HIP path")
-            K, k, nqp = ops.lqr_backward(C, c, F, n_state, n_ctrl, x=x, u=u, u_lower=lo, u_upper=hi,
-                                         u_zero_I=u_zero_I, want_nqp=lo is not None)
+            K, k, nqp = sweep(C, c, F, x, u, want_nqp=lo is not None)
             if m_id == N.MODEL_LINDX:
                 th, Fd, fd = None, true_dynamics.F, true_dynamics.f
                 if fd is not None and fd.nelement() == 0:
@@ -60,8 +70,9 @@ def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta
             else:
                 th, Fd, fd = ops.theta_of(true_dynamics, x_init), None, None
             Ct, ct = true_cost
+            flo, fhi = (lo, hi) if delta_u is None else ops.delta_u_rollout_bounds(lo, hi, u, delta_u)
             nx, nu, costs, du_sq, alphas = ops.lqr_forward(
-                m_id, th, x_init, Ct, ct, x, u, K, k, F=Fd, f=fd, u_lower=lo, u_upper=hi, u_zero_I=u_zero_I,
+                m_id, th, x_init, Ct, ct, x, u, K, k, F=Fd, f=fd, u_lower=flo, u_upper=fhi, u_zero_I=zI,
                 linesearch_decay=linesearch_decay, max_linesearch_iter=max_linesearch_iter)
             full_du_norm = ops.quirk_norm(du_sq)
             n_qp = int(nqp.max().item()) if nqp is not None else 0

@@ -31,8 +31,7 @@ class MPC(Module):
         super().__init__()
         assert (u_lower is None) == (u_upper is None)
         assert max_linesearch_iter > 0
-        if u_zero_I is not None:
-            raise NotImplementedError("dilqr: MPC(u_zero_I=...) — the mask is internal to the adjoint engine")
+        self.u_zero_I = None if u_zero_I is None else u_zero_I.detach()
         self.delta_u, self.slew_rate_penalty, self.prev_ctrl = delta_u, slew_rate_penalty, prev_ctrl
         self.n_state, self.n_ctrl, self.T = n_state, n_ctrl, T
         self.u_lower = u_lower if (u_lower is None or isinstance(u_lower, float)) else u_lower.detach()
@@ -79,16 +78,17 @@ class MPC(Module):
                                        u_lower=self.u_lower, u_upper=self.u_upper, lqr_iter=self.lqr_iter,
                                        eps=self.eps, linesearch_decay=self.linesearch_decay,
                                        max_linesearch_iter=self.max_linesearch_iter,
-                                       not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps)
+                                       not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps,
+                                       u_zero_I=self.u_zero_I)
         x, u, costs, full_du_norm = ws.best_x, ws.best_u, ws.best_cost, ws.best_du
         if torch.is_grad_enabled() and self.backprop:
             if lin:
                 F, f = dx.F, (dx.f if dx.f is not None else torch.empty(0, device=x.device))
             else:
                 F, f = ops.linearize(model_id, theta, x, u)
-            step = LQRStep(n, m, T, u_lower=self.u_lower, u_upper=self.u_upper, true_cost=QuadCost(C, c),
-                           true_dynamics=dx, current_x=x, current_u=u, back_eps=self.back_eps,
-                           no_op_forward=True)
+            step = LQRStep(n, m, T, u_lower=self.u_lower, u_upper=self.u_upper, u_zero_I=self.u_zero_I,
+                           true_cost=QuadCost(C, c), true_dynamics=dx, current_x=x, current_u=u,
+                           back_eps=self.back_eps, no_op_forward=True)
             x, u = step(x_init, C, c, F, f)
         if self.detach_unconverged and float(full_du_norm.max()) > self.eps:    # mpc.py:321-334
             if self.exit_unconverged:

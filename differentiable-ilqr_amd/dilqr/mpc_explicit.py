@@ -53,7 +53,7 @@ class MPC(Module):
         self.n_state, self.n_ctrl, self.T = n_state, n_ctrl, T
         self.u_lower = u_lower if (u_lower is None or isinstance(u_lower, float)) else u_lower.detach()
         self.u_upper = u_upper if (u_upper is None or isinstance(u_upper, float)) else u_upper.detach()
-        self.u_zero_I = u_zero_I
+        self.u_zero_I = None if u_zero_I is None else u_zero_I.detach()
         self.u_init = None if u_init is None else u_init.detach()
         self.lqr_iter = lqr_iter
         self.grad_method = grad_method
@@ -71,14 +71,13 @@ class MPC(Module):
         self.best_cost_eps = best_cost_eps
         self.slew_rate_penalty = slew_rate_penalty
         self.prev_ctrl = prev_ctrl
-        if u_zero_I is not None:
-            raise NotImplementedError("dilqr: MPC(u_zero_I=...) — the mask is internal to the adjoint engine")
         if grad_method == GradMethods.ANALYTIC_CHECK:
             raise NotImplementedError("dilqr: ANALYTIC_CHECK is disabled in the reference too (mpc_explicit.py:578)")
 
     def fused(self, cost, dx):
-        """The whole loop in the fused HIP kernels: an env_dx model with its
-        analytic Jacobian, a quadratic cost, no slew-rate penalty / delta_u.
+        """The whole loop on device in HIP kernels: an env_dx model with its
+        analytic Jacobian, a quadratic cost, no slew-rate penalty / delta_u
+        (the fused iteration; with a u_zero_I mask the unfused kernels).
         Anything else runs the generic loop (dilqr.generic)."""
         return (isinstance(cost, QuadCost) and getattr(dx, "model_id", None) is not None
                 and self.grad_method == GradMethods.ANALYTIC and self.slew_rate_penalty is None
@@ -100,11 +99,21 @@ class MPC(Module):
         theta = ops.theta_of(dx, x_init)
         Cd, cd = C.detach().contiguous(), c.detach().contiguous()
         with torch.no_grad():
-            x, u, costs, full_du_norm, sv = ops.mpc_solve(
-                model_id, theta, x_init.detach(), Cd, cd, T, u_init=self.u_init, u_lower=self.u_lower,
-                u_upper=self.u_upper, lqr_iter=self.lqr_iter, eps=self.eps,
-                linesearch_decay=self.linesearch_decay, max_linesearch_iter=self.max_linesearch_iter,
-                not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps)
+            if self.u_zero_I is None:
+                x, u, costs, full_du_norm, sv = ops.mpc_solve(
+                    model_id, theta, x_init.detach(), Cd, cd, T, u_init=self.u_init, u_lower=self.u_lower,
+                    u_upper=self.u_upper, lqr_iter=self.lqr_iter, eps=self.eps,
+                    linesearch_decay=self.linesearch_decay, max_linesearch_iter=self.max_linesearch_iter,
+                    not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps)
+            else:
+                # controls held at zero (mpc_explicit.py:369, 452 -> LQRStep u_zero_I):
+                # the unfused kernels take the mask (masked gain solve, zeroed rollout)
+                sv = ops.mpc_solve_unfused(
+                    model_id, theta, x_init.detach(), Cd, cd, T, u_init=self.u_init, u_lower=self.u_lower,
+                    u_upper=self.u_upper, lqr_iter=self.lqr_iter, eps=self.eps,
+                    linesearch_decay=self.linesearch_decay, max_linesearch_iter=self.max_linesearch_iter,
+                    not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps, u_zero_I=self.u_zero_I)
+                x, u, costs, full_du_norm = sv.best_x, sv.best_u, sv.best_cost, sv.best_du
         self.last_solve = sv
 
         need_grad = torch.is_grad_enabled() and self.backprop and (
@@ -115,9 +124,9 @@ class MPC(Module):
             # to the implicit backward through a no-op LQR step.
             F, f = ops.linearize(model_id, theta, x, u)
             th = dx.params if isinstance(dx.params, torch.Tensor) else torch.tensor(dx.params)
-            step = LQRStep(n, m, T, u_lower=self.u_lower, u_upper=self.u_upper, true_cost=QuadCost(C, c),
-                           true_dynamics=dx, current_x=x, current_u=u, back_eps=self.back_eps,
-                           no_op_forward=True)
+            step = LQRStep(n, m, T, u_lower=self.u_lower, u_upper=self.u_upper, u_zero_I=self.u_zero_I,
+                           true_cost=QuadCost(C, c), true_dynamics=dx, current_x=x, current_u=u,
+                           back_eps=self.back_eps, no_op_forward=True)
             x, u = step(x_init, C, c, F, f, th)
         return self._detach_unconverged(x, u, costs, full_du_norm)
 

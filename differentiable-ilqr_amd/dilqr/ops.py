@@ -71,6 +71,39 @@ def lqr_backward(C, c, F, n, m, x=None, u=None, u_lower=None, u_upper=None, u_ze
     return K, k, nqp
 
 
+def c_back(C, c, x, u):
+    """Delta-space linear term C_t tau_t + c_t (lqr_step_explicit.py:630-636),
+    for the callers that hand the sweep relative bounds (delta_u)."""
+    tau = torch.cat((x, u), -1)
+    return (C @ tau.unsqueeze(-1)).squeeze(-1) + c
+
+
+def _full(v, like):
+    return v if isinstance(v, torch.Tensor) else torch.full_like(like, float(v))
+
+
+def delta_u_sweep_bounds(u_lower, u_upper, u, delta_u):
+    """The sweep's box in delta space with the delta_u trust region,
+    lqr_step_explicit.py:132-135: lb = lower - u_t, ub = upper - u_t, then
+    lb[lb < -delta_u] = -delta_u, ub[ub > delta_u] = delta_u (exact values)."""
+    lb = _full(u_lower, u) - u
+    ub = _full(u_upper, u) - u
+    lb = torch.where(lb < -delta_u, torch.full_like(lb, -delta_u), lb)
+    ub = torch.where(ub > delta_u, torch.full_like(ub, delta_u), ub)
+    return lb.contiguous(), ub.contiguous()
+
+
+def delta_u_rollout_bounds(u_lower, u_upper, u, delta_u):
+    """The rollout's clamp with the delta_u trust region, lqr_step_explicit.py:
+    205-213: lb = u_t - delta_u raised to lower, ub = u_t + delta_u cut to upper."""
+    lb = u - delta_u
+    ub = u + delta_u
+    lo, hi = _full(u_lower, u), _full(u_upper, u)
+    lb = torch.where(lb < lo, lo, lb)
+    ub = torch.where(ub > hi, hi, ub)
+    return lb.contiguous(), ub.contiguous()
+
+
 def lqr_forward(model_id, theta, x_init, C, c, x, u, K, k, F=None, f=None, u_lower=None, u_upper=None,
                 u_zero_I=None, linesearch_decay=0.2, max_linesearch_iter=10):
     """lqr_forward (lqr_step_explicit.py:166-263): returns new_x, new_u, costs [B],
@@ -266,10 +299,12 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     m = C.shape[-1] - n
     x_init, C, c = _f32(x_init), _f32(C), _f32(c)
     # the stop rule (max full_du_norm < eps or n_not_improved > lim) cannot fire:
-    # one launch per iteration, best_du formed at the end (same values)
-    # (the per-iteration du planes are kept: up to 2 GiB of them)
+    # one launch per iteration, best_du formed at the end (same values).  The
+    # per-iteration du planes are kept, so this mode is taken only while they
+    # stay small: at most 1/16 of the free device memory and 2 GiB
+    plane_bytes = 4 * lqr_iter * T * m * B
     fixed = (lqr_iter >= 1 and eps <= 0 and not_improved_lim >= lqr_iter
-             and 4 * lqr_iter * T * m * B <= 2 ** 31)
+             and plane_bytes <= min(2 ** 31, torch.cuda.mem_get_info(x_init.device)[0] // 16))
     sv = MPCSolve(T, B, n, m, x_init.device, fixed_iters=lqr_iter if fixed else None)
     sv.begin(model_id, theta, x_init, u_init)
     bounds, keep = N.make_bounds(u_lower, u_upper)
@@ -314,10 +349,14 @@ def lqr_adjoint(C, c, F, x, u, dl_dx, dl_du, u_lower=None, u_upper=None, m_solve
 
 def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=None, u_lower=None,
                       u_upper=None, lqr_iter=10, eps=1e-7, linesearch_decay=0.2, max_linesearch_iter=10,
-                      not_improved_lim=5, best_cost_eps=1e-4, check_every=8):
+                      not_improved_lim=5, best_cost_eps=1e-4, check_every=8, u_zero_I=None):
     """The same outer loop with the unfused kernels (linearise -> F in HBM ->
     Riccati -> rollout/line search).  Used for LinDx dynamics (classic mpc.MPC,
-    the adjoint engines) and to cross-check the fused iteration."""
+    the adjoint engines), MPC(u_zero_I=...) and to cross-check the fused
+    iteration.  u_zero_I [T,B,m] (bool): controls held at zero — the sweep's
+    masked solve when unconstrained (lqr_step_explicit.py:98-129; with bounds
+    the reference's pnqp branch ignores the mask) and zeroed in every rollout
+    before the clamp (199-200)."""
     B, n = x_init.shape
     m = C.shape[-1] - n
     dev = x_init.device
@@ -331,6 +370,9 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
             u0 = u0.unsqueeze(1).expand(T, B, m)
         ws.ua.copy_(u0)
     s = N.stream(dev)
+    zI = None if u_zero_I is None else u_zero_I.to(device=dev, dtype=torch.uint8).contiguous()
+    if zI is not None and tuple(zI.shape) != (T, B, m):
+        raise ValueError(f"u_zero_I: expected [T, B, m] = {(T, B, m)}, got {tuple(zI.shape)}")
     N.call("dilqr_rollout_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f), N.ptr(x_init),
            N.ptr(ws.ua), N.ptr(ws.xa), s)
     for i in range(lqr_iter):
@@ -338,13 +380,14 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
             Fi, fi = F, f
         else:
             Fi, fi = linearize(model_id, theta, ws.xa, ws.ua)
-        K, k, _ = lqr_backward(C, c, Fi, n, m, x=ws.xa, u=ws.ua, u_lower=u_lower, u_upper=u_upper)
+        K, k, _ = lqr_backward(C, c, Fi, n, m, x=ws.xa, u=ws.ua, u_lower=u_lower, u_upper=u_upper,
+                               u_zero_I=zI if u_lower is None else None)
         bounds, keep = N.make_bounds(u_lower, u_upper)
         # from iteration 1 the old cost is the previous line search's value for
         # the accepted candidate (ws.cost), as the fused MPC kernel takes it
         prev = (N.ptr(ws.cost) if i > 0 and model_id in (N.MODEL_PENDULUM, N.MODEL_CARTPOLE) else None)
         N.call("dilqr_lqr_forward_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f),
-               N.ptr(x_init), N.ptr(C), N.ptr(c), N.ptr(ws.xa), N.ptr(ws.ua), N.ptr(K), N.ptr(k), bounds, None,
+               N.ptr(x_init), N.ptr(C), N.ptr(c), N.ptr(ws.xa), N.ptr(ws.ua), N.ptr(K), N.ptr(k), bounds, N.ptr(zI),
                float(linesearch_decay), int(max_linesearch_iter), N.ptr(ws.xb), N.ptr(ws.ub), N.ptr(ws.cost),
                N.ptr(ws.du_sq), N.ptr(ws.alpha), prev, s)
         N.call("dilqr_mpc_update_best_f32", n, m, T, B, int(i == 0), float(best_cost_eps), float(eps),

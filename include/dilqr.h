@@ -61,8 +61,13 @@ typedef struct dilqr_bounds {
   const float* hi_t;             /* [T,B,m] or NULL                              */
 } dilqr_bounds;
 
-/* Library version (for the loader's sanity check). */
+/* Library version (for the loader's sanity check): 5. */
 int dilqr_version(void);
+
+/* Build id: the first 16 hex digits of the sha256 of the sources the library
+   was built from (differentiable-ilqr_amd/Makefile BUILD_ID; the loader
+   dilqr/_native.py recomputes it from the tree and refuses a mismatch). */
+const char* dilqr_build_id(void);
 
 /* Number of parameters theta of a model (4 for cartpole), or -1. */
 int dilqr_model_num_params(int model);
@@ -102,7 +107,9 @@ int dilqr_linearize_f32(int model, int T, int B, const float* theta, const float
 /* Backward Riccati sweep in delta space: lqr_backward, lqr_step_explicit.py:54-162
    (with the c_back of 630-636 fused: c_back_t = C_t [x_t;u_t] + c_t; pass
    x = NULL to give c_back directly in c — u may then still be given, it only
-   shifts the box bounds (lb = lower - u_t)).  Bounded problems
+   shifts the box bounds (lb = lower - u_t); with u = NULL too the bounds are
+   taken as already relative, lb = lower: the delta_u trust region clips them
+   to +-delta_u, lqr_step_explicit.py:132-135).  Bounded problems
    run pnqp (pnqp.py:5-82) per step, warm-started from the later step.
    u_zero_I [T,B,m] (uint8, nullable): the masked solve of
    lqr_step_backup.py:210-232 used by the adjoint engines.
@@ -121,7 +128,9 @@ int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const flo
    old_cost [B] (nullable): the current trajectory's cost when the caller has
    it (an MPC loop: its previous line search's value for the accepted
    candidate), else formed from x, u (lqr_step_explicit.py:171); one lane per
-   problem models and LINDX d <= 8 only (DILQR_E_MODE otherwise). */
+   problem models and LINDX d <= 8 only (DILQR_E_MODE otherwise).  old_cost
+   may alias cost (each problem's old cost is read before its new cost is
+   written). */
 int dilqr_lqr_forward_f32(int model, int n, int m, int T, int B, const float* theta,
                           const float* F, const float* f, const float* x_init,
                           const float* C, const float* c, const float* x,
@@ -222,8 +231,8 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
 /* Caller-owned device buffers of one solve.  Xs and Us hold four trajectories
    per problem: for the pendulum and cartpole Xs is [4,T,B,n+m] records
    [x_t; u_t] (a lane moves its record with two wide accesses) and Us is unused
-   (pass Xs); for rocket Xs is [4,T,B,n] and Us [4,T,B,m].  The caller puts
-   u_init (or zeros) into slot 0's u before begin.  slot [2,B] (uint8) the indices of each
+   (pass Xs); for rocket Xs is [4,T,B,n] and Us [4,T,B,m].  begin writes slot
+   0 itself (see dilqr_mpc_begin_f32).  slot [2,B] (uint8) the indices of each
    problem's current and best one.  The line search's two candidates roll out
    into the two free slots, so accepting a step size or taking an iterate as
    the new best (mpc_explicit.py:277-283) moves no data.
@@ -255,9 +264,11 @@ typedef struct dilqr_mpc_state {
   int* best_iter;        /* [B], fixed-count solves only (NULL otherwise) */
 } dilqr_mpc_state;
 
-/* Start a solve: slot 0 = (get_traj(u), u) with u = u_init ([T,B,m], the
-   caller's controls) or zeros when u_init is NULL; slots/ctrl reset
-   (mpc_explicit.py:228-249, util.py:104-127). */
+/* Start a solve: slot 0 = (get_traj(u), u) with u = u_init or zeros when
+   u_init is NULL; slots/ctrl reset (mpc_explicit.py:228-249, util.py:104-127).
+   u_init: the caller's controls, fp32 [T,B,m] contiguous (time-major, the
+   reference's layout), read once with scalar loads, so 4-byte alignment
+   suffices (checked; the 16-byte rule above does not apply to it). */
 int dilqr_mpc_packed_cost_floats(int n, int m);
 int dilqr_mpc_begin_f32(int model, int T, int B, const float* theta, const float* x_init,
                         const float* u_init, dilqr_mpc_state st, void* stream);
@@ -293,8 +304,8 @@ int dilqr_mpc_stop_rule_f32(int T, int m, int B, int iteration, dilqr_mpc_state 
    keeps in best_iter[B] the last iteration that took the best-iterate branch
    (mpc_explicit.py:277-283).  dilqr_mpc_finish_fixed_f32 then forms best_du
    from those planes (the quirk rows, lqr_step_explicit.py:245-247, bit for bit
-   the per-iteration rule's values) and sets ctrl[].iter; full_du_norm is not
-   maintained in this mode. */
+   the per-iteration rule's values), full_du_norm from the last iteration's
+   plane (what the per-iteration rule leaves there) and sets ctrl[].iter. */
 int dilqr_mpc_iterate_fixed_f32(int model, int T, int B, const float* theta, const float* x_init,
                                 const float* C, const float* c, dilqr_bounds bounds,
                                 float linesearch_decay, int max_linesearch_iter, int iteration,

@@ -14,7 +14,7 @@ HEADER = os.path.join(ROOT, "include", "dilqr.h")
 def header_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\bint\s+(dilqr_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(?:int|const char\s*\*)\s+(dilqr_\w+)\s*\(", src)))
 
 
 def test_header_declares_entry_points():
@@ -30,6 +30,15 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     # the python binding declares a signature for every header entry point
     assert sorted(_native.exported_symbols()) == header_functions()
+
+
+def test_build_id_matches_tree():
+    """The loaded library was built from the sources in this tree (the Makefile
+    stamps a hash of csrc/ + include/dilqr.h; _native.lib() refuses a mismatch)."""
+    from dilqr import _native
+    lib = _native.lib()
+    tree = _native.tree_build_id()
+    assert tree is not None and lib.dilqr_build_id().decode() == tree
 
 
 def test_version_and_model_table():

@@ -388,6 +388,8 @@ def test_fixed_count_solve_equals_stop_rule_path(golden, name):
     assert torch.equal(xa, xb) and torch.equal(ua, ub)
     assert torch.equal(a.best_cost, cost_b) and torch.equal(a.best_du, du_b)
     assert torch.isfinite(du_b).all()
+    # full_du_norm: the last iteration's quirk rows on both paths
+    assert torch.equal(a.full_du_norm, sv.full_du_norm)
 
 
 # ------------------------------------------------------------------ DiLQR implicit backward

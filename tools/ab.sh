@@ -3,6 +3,7 @@
 # every variant present), alternating, bench --kernels-only by default.
 # Usage: bash tools/ab.sh [rounds]; AB_CMD overrides the timed command.
 set -o pipefail
+export DILQR_SKIP_BUILD_ID=1   # the variants are built from other sources on purpose
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 L=differentiable-ilqr_amd/dilqr/libdilqr.so
 cp $L ab/.inplace.so
