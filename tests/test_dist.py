@@ -68,3 +68,43 @@ def test_shard_rows_cover_batch():
         rows = [bench.shard_rows(65536 * world, world, r) for r in range(world)]
         assert rows[0][0] == 0 and rows[-1][1] == 65536 * world
         assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
+
+
+@pytest.mark.gpu
+def test_bench_sharded_hip_path_equals_whole_batch(tmp_path):
+    """bench.py's N > 1 path on the HIP library: two ranks (torchrun, gloo for the
+    timing reduction, both on cuda:0) each solve their contiguous shard of the
+    generated batch; the shards' best trajectories and costs equal, bit for bit,
+    the whole-batch solve of the same problems (problems are independent, so no
+    collective is needed in the data path)."""
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    world, B_per, it = 2, 1024, 10
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(world), "--batch", str(B_per), "--steps", str(it), "--warmup", "0", "--lqr-iter", str(it),
+           "--no-secondary", "--no-cpu-baseline", "--dump", str(tmp_path)]
+    r = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import bench
+    from dilqr import ops
+    from dilqr import _native as N
+    x0_all, q, p = bench.make_problems(B_per * world)
+    dev = torch.device("cuda:0")
+    T, B = bench.T_HORIZON, B_per * world
+    x0 = torch.tensor(x0_all, device=dev)
+    C = torch.diag(torch.tensor(q)).repeat(T, B, 1, 1).to(dev).contiguous()
+    c = torch.tensor(p).repeat(T, B, 1).to(dev).contiguous()
+    theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
+    x, u, cost, _, _ = ops.mpc_solve(N.MODEL_CARTPOLE, theta, x0, C, c, T, lqr_iter=it, eps=0.0,
+                                     linesearch_decay=0.5, max_linesearch_iter=2, not_improved_lim=10 ** 9)
+    for rank in range(world):
+        sh = torch.load(tmp_path / f"shard{rank}.pt", weights_only=True)
+        lo, hi = sh["rows"]
+        assert (lo, hi) == bench.shard_rows(B, world, rank)
+        assert torch.equal(sh["u"], u[:, lo:hi].cpu()) and torch.equal(sh["x"], x[:, lo:hi].cpu())
+        assert torch.equal(sh["cost"], cost[lo:hi].cpu())

@@ -8,7 +8,8 @@ mkdir -p $OUT
 STEPS="${STEPS:-all}"
 make -C differentiable-ilqr_amd -j16 > $OUT/build.log 2>&1 || { echo "build failed"; tail -20 $OUT/build.log; exit 1; }
 if [[ "$STEPS" == *all* || "$STEPS" == *test* ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -rfE ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -rfE -s --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+      > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -30 $OUT/pytest_gpu.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi

@@ -1,53 +1,75 @@
 #!/usr/bin/env python3
-"""Summarise the PMC passes of tools/profile_pmc.sh into profiles/<round>/pmc_summary.json
-and profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
+"""Summarise the PMC passes of tools/profile_pmc.sh into
+profiles/<round>/pmc_summary.json (every kernel instantiation seen, median
+launch per counter) and profiles/pmc_traffic.json (read by bench.py for each
+roofline's `traffic`).
 
-Fabric bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB counters).  The
-factors are calibrated, per access pattern, by tools/microbench/fetch_calib.hip
-(tools/fetch_calib.sh; profiles/r02/pmc_calibration.json): FETCH_SIZE = 0.50 x
-bytes for 4-B/lane coalesced, 16-B/lane coalesced and 144-B-record-per-lane
-reads, WRITE_SIZE = 1.00 x bytes for 4-B and 16-B/lane stores — the patterns of
-the hot kernels (the MPC slots' component planes, the float4 planes, the
-caller's C records).  The counters sit on the L2's memory side, so MALL
-(Infinity Cache) hits are included: the figure is L2-miss traffic, an upper
-bound on HBM traffic.  Raw counters are kept next to the corrected figure."""
-import subprocess
+HBM-side bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB counters).  On
+gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads
+(MI355X_MICROARCH.md, HBM section); tools/microbench/fetch_calib.hip measured
+the same 0.50 for the 4-B/lane, 16-B/lane and 144-B-record-per-lane reads of
+these kernels and WRITE_SIZE = 1.00 x bytes for their stores
+(profiles/r02/pmc_calibration.json).  The counters sit on the L2's memory side,
+so Infinity-Cache hits count: an upper bound on HBM traffic.  SQ_* cycle
+counters are quad-cycles per wave; ratios to SQ_WAVE_CYCLES are fractions of
+wave lifetime."""
 import collections
 import csv
 import json
 import os
+import re
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def short(name):
-    for key in ("k_mpc_iterate", "k_ilqr_iterate", "k_lqr_backward", "k_mpc_norm_control", "k_implicit_backward",
-                "k_lqr_forward", "k_lqr_adjoint"):
-        if key in name:
-            if key == "k_mpc_iterate" and name.split("(")[0].rstrip().endswith("true>"):
-                key += "<first>"                      # iteration 0's own instantiation (FIRST = true)
-            return key + ("<box>" if "Li3EE" in name else "")
-    return None
+def signature(name):
+    """'void dilqr::k_mpc_iterate<dilqr::Cartpole, 0, true, false>(int, ...)' ->
+    'k_mpc_iterate<Cartpole, 0, true, false>' (one key per instantiation)."""
+    head = name.split("(")[0].strip()
+    head = re.sub(r"^void\s+", "", head).replace("dilqr::gen::", "").replace("dilqr::", "")
+    return head
+
+
+def derived(c):
+    out = {}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["fetch_bytes_raw"] = c["FETCH_SIZE"] * 1024
+        out["write_bytes_raw"] = c["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+    w = c.get("SQ_WAVE_CYCLES")
+    if w:
+        for k, name in (("SQ_ACTIVE_INST_VALU", "valu_busy"), ("SQ_WAIT_ANY", "waitcnt_stall"),
+                        ("SQ_WAIT_INST_ANY", "issue_stall"), ("SQ_ACTIVE_INST_VMEM", "vmem_busy"),
+                        ("SQ_ACTIVE_INST_LDS", "lds_busy")):
+            if k in c:
+                out[name] = c[k] / w
+    if c.get("SQ_WAVES"):
+        for k, name in (("SQ_INSTS_VALU", "valu_instr_per_wave"), ("SQ_INSTS_LDS", "lds_instr_per_wave"),
+                        ("SQ_INSTS_SALU", "salu_instr_per_wave"), ("SQ_INSTS_VMEM_RD", "vmem_rd_instr_per_wave")):
+            if k in c:
+                out[name] = c[k] / c["SQ_WAVES"]
+    return out
 
 
 def main(pmc_dir, round_tag):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for p in sorted(os.listdir(pmc_dir)):
-        f = os.path.join(pmc_dir, p, "run_counter_collection.csv")
-        if not os.path.exists(f):
+        d = os.path.join(pmc_dir, p)
+        if not os.path.isdir(d):
             continue
-        for r in csv.DictReader(open(f)):
-            k = short(r["Kernel_Name"])
-            if k:
-                agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for f in (os.path.join(d, "run_counter_collection.csv"),):
+            if not os.path.exists(f):
+                continue
+            for r in csv.DictReader(open(f)):
+                agg[signature(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
-    for k, cs in agg.items():
-        out[k] = {c: sorted(v)[len(v) // 2] for c, v in cs.items()}   # median launch
-        if "FETCH_SIZE" in out[k] and "WRITE_SIZE" in out[k]:
-            out[k]["fetch_bytes_raw"] = out[k]["FETCH_SIZE"] * 1024
-            out[k]["write_bytes_raw"] = out[k]["WRITE_SIZE"] * 1024
-            out[k]["hbm_bytes_per_launch"] = (2 * out[k]["FETCH_SIZE"] + out[k]["WRITE_SIZE"]) * 1024
+    for k, cs in sorted(agg.items()):
+        med = {c: sorted(v)[len(v) // 2] for c, v in cs.items()}        # median launch
+        med["launches"] = max(len(v) for v in cs.values())
+        med.update(derived(med))
+        out[k] = med
     os.makedirs(os.path.join(ROOT, "profiles", round_tag), exist_ok=True)
     json.dump(out, open(os.path.join(ROOT, "profiles", round_tag, "pmc_summary.json"), "w"), indent=1)
     try:
@@ -55,23 +77,18 @@ def main(pmc_dir, round_tag):
                               text=True).stdout.strip()
     except OSError:
         head = "?"
-    t = {"note": "L2-miss (fabric) bytes per launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 from rocprofv3 --pmc "
-                 "(factors calibrated per access pattern: profiles/r02/pmc_calibration.json), "
-                 f"profiles/{round_tag}/pmc_summary.json; cartpole T=25 B=65536",
-         "measured_at_commit": head}
-    for k in ("k_ilqr_iterate", "k_mpc_iterate", "k_lqr_backward"):
-        if k in out and "hbm_bytes_per_launch" in out[k]:
-            t[k + "_bytes_per_launch"] = out[k]["hbm_bytes_per_launch"]
-            t[k + "_raw"] = {"FETCH_SIZE_KiB": out[k]["FETCH_SIZE"], "WRITE_SIZE_KiB": out[k]["WRITE_SIZE"]}
-            if "SQ_WAVE_CYCLES" in out[k] and "SQ_ACTIVE_INST_VALU" in out[k]:
-                w = out[k]["SQ_WAVE_CYCLES"]
-                t[k + "_issue"] = {"valu_busy": out[k]["SQ_ACTIVE_INST_VALU"] / w,
-                                   "waitcnt_stall": out[k].get("SQ_WAIT_ANY", 0.0) / w,
-                                   "valu_instr_per_wave": out[k]["SQ_INSTS_VALU"] / out[k]["SQ_WAVES"]}
+    keep = ("hbm_bytes_per_launch", "fetch_bytes_raw", "write_bytes_raw", "valu_busy", "waitcnt_stall", "issue_stall",
+            "lds_busy", "valu_instr_per_wave", "lds_instr_per_wave")
+    t = {"note": "per kernel instantiation, median launch: HBM-side bytes per launch = (2*FETCH_SIZE + "
+                 "WRITE_SIZE)*1024 (gfx950 FETCH_SIZE = half the bytes, MI355X_MICROARCH.md; "
+                 f"profiles/r02/pmc_calibration.json), issue fractions of SQ_WAVE_CYCLES; profiles/{round_tag}/"
+                 "pmc_summary.json", "measured_at_commit": head,
+         "kernels": {k: {f: v[f] for f in keep if f in v} for k, v in out.items()}}
     json.dump(t, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(t, indent=1))
+    for k, v in t["kernels"].items():
+        print(k, json.dumps({f: round(x, 4) if isinstance(x, float) and x < 100 else x for f, x in v.items()}))
 
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc"),
-         sys.argv[2] if len(sys.argv) > 2 else "r02")
+         sys.argv[2] if len(sys.argv) > 2 else "r03")
