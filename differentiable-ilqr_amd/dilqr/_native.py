@@ -69,6 +69,9 @@ SIGNATURES = {
     "dilqr_mpc_iterate_fixed_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, MpcState, _vp], _i),
     "dilqr_mpc_finish_fixed_f32": ([_i, _i, _i, _i, MpcState, _vp], _i),
     "dilqr_mpc_gather_best_f32": ([_i, _i, _i, _i, MpcState, _vp, _vp, _vp], _i),
+    "dilqr_get_matrices_f32": ([_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "dilqr_grad_input_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                              _vp], _i),
     "dilqr_implicit_backward_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds, _vp, _vp, _vp,
                                      _vp, _vp], _i),
 }

@@ -66,6 +66,45 @@ class HipDynamics(nn.Module):
                N.ptr(D), N.stream(x.device))
         return D
 
+    def get_matrices(self, x, u):
+        """(D, D_grad_params, D_grad_x, D_grad_u, x_grad_theta, x_grad_xtm1,
+        x_grad_utm1) per row (cartpole.py:105-716, pendulum.py:152-382,
+        rocket.py:258-261): one HIP kernel, dilqr_get_matrices_f32."""
+        x = x.detach().float().contiguous()
+        u = u.detach().float().contiguous()
+        Nr, n, m = x.shape[0], self.n_state, self.n_ctrl
+        d, p = n + m, N.lib().dilqr_model_num_params(self.model_id)
+        dev = x.device
+        outs = [torch.empty(Nr, *sh, device=dev) for sh in ((n, d), (n, d, p), (n, d, n), (n, d, m), (n, p),
+                                                              (n, n), (n, m))]
+        N.call("dilqr_get_matrices_f32", self.model_id, Nr, N.ptr(self._theta(x)), N.ptr(x), N.ptr(u),
+               *[N.ptr(o) for o in outs], N.stream(dev))
+        return tuple(outs)
+
+    def grad_input(self, X, U, K=None):
+        """The closed-loop total derivatives of the reference's grad_input
+        (cartpole.py:717-788, pendulum.py:383-443, rocket.py:263-323):
+        (grad_D [T-1,B,n,d,p], grad_d [T-1,B,n,p], D_x [T-1,B,n,d,n],
+        D_u [T-1,B,n,d,m], D [T-1,B,n,d], d_x [T-1,B,n,n], d_u [T-1,B,n,m]).
+        K [T,B,m,n] is consumed as K[t] (the order the caller stacks it; the
+        implicit backward passes the reversed Riccati stack); None = zeros."""
+        T, B, n = X.shape
+        m = U.shape[2]
+        d, p = n + m, N.lib().dilqr_model_num_params(self.model_id)
+        dev = X.device
+        Xc, Uc = X.detach().float().contiguous(), U.detach().float().contiguous()
+        D, Dp, Dx, Du, xth, xx, xu = self.get_matrices(Xc.view(T * B, n), Uc.view(T * B, m))
+        Kc = None if K is None else torch.as_tensor(K).detach().to(device=dev, dtype=torch.float32).contiguous()
+        Tm = max(T - 1, 0)
+        gD = torch.empty(Tm, B, n, d, p, device=dev)
+        gd = torch.empty(Tm, B, n, p, device=dev)
+        dX = torch.empty(Tm, B, n, n, device=dev)
+        dU = torch.empty(Tm, B, n, m, device=dev)
+        N.call("dilqr_grad_input_f32", self.model_id, T, B, N.ptr(Xc), N.ptr(Uc), N.ptr(Kc),
+               *[N.ptr(a) for a in (D, Dp, Dx, Du, xth, xx, xu, gD, gd, dX, dU)], N.stream(dev))
+        sh = lambda a: a.view(T, B, *a.shape[1:])[:Tm]  # noqa: E731
+        return gD, gd, sh(Dx), sh(Du), sh(D), dX, dU
+
     def get_true_obj(self):
         q = torch.cat((self.goal_weights, self.ctrl_penalty * torch.ones(self.n_ctrl)))
         px = -torch.sqrt(self.goal_weights) * self.goal_state

@@ -227,6 +227,30 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta,
                                 const float* dl_du, dilqr_bounds bounds, float* ws,
                                 float* dC, float* dc, float* dtheta, void* stream);
 
+/* ---- the model protocol's second-order API (not on the solver's path) ---- */
+
+/* get_matrices: cartpole.py:105-716, pendulum.py:152-382, rocket.py:258-261
+   (+ its build_batched_* tables, 541-820).  Per row of x [N,n], u [N,m] (the
+   unclamped u): D [N,n,d] (= get_linear_dyn), D_params [N,n,d,p], D_x
+   [N,n,d,n], D_u [N,n,d,m], x_theta [N,n,p], x_xtm1 [N,n,n], x_utm1 [N,n,m],
+   with the reference's closed forms where they differ from the derivative
+   (cartpole: D_params[4,3..5,*] and x_xtm1[0,0] = 0; rocket: the builder
+   tables).  Zero-fills the sparse arrays on `stream` first. */
+int dilqr_get_matrices_f32(int model, int N, const float* theta, const float* x,
+                           const float* u, float* D, float* Dp, float* Dx, float* Du,
+                           float* x_theta, float* x_xtm1, float* x_utm1, void* stream);
+
+/* grad_input: cartpole.py:717-788, pendulum.py:383-443, rocket.py:263-323.
+   X [T,B,n], U [T,B,m], K [T,B,m,n] consumed as K[t] (NULL = zeros), and
+   dilqr_get_matrices_f32's outputs for the T*B rows.  Outputs grad_D
+   [T-1,B,n,d,p], grad_d [T-1,B,n,p], d_x = -D_x tau [T-1,B,n,n], d_u = -D_u tau
+   [T-1,B,n,m] (the 7-tuple's other members are get_matrices' D_x, D_u, D). */
+int dilqr_grad_input_f32(int model, int T, int B, const float* X, const float* U,
+                         const float* K, const float* D, const float* Dp, const float* Dx,
+                         const float* Du, const float* x_theta, const float* x_xtm1,
+                         const float* x_utm1, float* grad_D, float* grad_d, float* d_x,
+                         float* d_u, void* stream);
+
 /* ---- the device-resident MPC loop with per-problem trajectory slots ------ */
 /* Caller-owned device buffers of one solve.  Xs and Us hold four trajectories
    per problem: for the pendulum and cartpole Xs is [4,T,B,n+m] records

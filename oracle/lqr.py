@@ -39,18 +39,36 @@ def _slice(v, sl):
     return v if np.ndim(v) == 0 else v[sl]
 
 
-def pnqp(H, q, lower, upper, x_init=None, n_iter=20, per_problem=False):
+def _note(margins, key, vals):
+    """margins[key] = elementwise min(margins[key], vals) (per problem)."""
+    if margins is None:
+        return
+    vals = np.asarray(vals, np.float64)
+    margins[key] = vals if key not in margins else np.minimum(margins[key], vals)
+
+
+def pnqp(H, q, lower, upper, x_init=None, n_iter=20, per_problem=False, margins=None):
     """Projected-Newton box QP, pnqp.py:5-82.
 
     Returns (x [B,m], H_free [B,m,m] (the masked matrix whose LU/inverse the
     reference returns), If [B,m] free mask, n_iter_done).
     With per_problem=True, n_iter_done is an int array [B].
+
+    margins (dict, per_problem only): per problem, the smallest distance of any
+    of its discrete decisions from its threshold — the clamp of a candidate
+    (|x - bound|, relative), the clamped-set sign test (|g_i| at a bound), the
+    stop test (| ||dx|| - 1e-4 |) and the Armijo test (|armijo - GAMMA|) —
+    so a test can tell a near-tie decision (which fp32 may take the other way)
+    from real error.  Key 'pnqp'.
     """
     if per_problem:
         B = H.shape[0]
+        mb = [dict() if margins is not None else None for _ in range(B)]
         outs = [pnqp(H[b:b + 1], q[b:b + 1], _slice(lower, slice(b, b + 1)),
                      _slice(upper, slice(b, b + 1)),
-                     None if x_init is None else x_init[b:b + 1], n_iter) for b in range(B)]
+                     None if x_init is None else x_init[b:b + 1], n_iter, margins=mb[b]) for b in range(B)]
+        if margins is not None:
+            _note(margins, "pnqp", [m_.get("pnqp", [np.inf])[0] for m_ in mb])
         return (np.concatenate([o[0] for o in outs]), np.concatenate([o[1] for o in outs]),
                 np.concatenate([o[2] for o in outs]), np.array([o[3] for o in outs]))
     dt = H.dtype
@@ -65,11 +83,20 @@ def pnqp(H, q, lower, upper, x_init=None, n_iter=20, per_problem=False):
             x_init = -(1. / H[:, :, 0]) * q
         else:
             x_init = -np.linalg.solve(H, q[..., None])[..., 0]
+    def bound_gap(z):                                    # distance of z from the nearer bound
+        sc = np.maximum(1.0, np.abs(z))
+        return np.min(np.minimum(np.abs(z - lower), np.abs(z - upper)) / sc, axis=1)
+
+    if margins is not None:
+        _note(margins, "pnqp", bound_gap(x_init))
     x = eclamp(x_init, lower, upper)
 
     H_ = If = None
     for i in range(n_iter):                              # pnqp.py:28-78
         g = bmv(H, x) + q
+        if margins is not None:
+            at = (x == lower) | (x == upper)
+            _note(margins, "pnqp", np.min(np.where(at, np.abs(g), np.inf), axis=1))
         Ic = (((x == lower) & (g > 0)) | ((x == upper) & (g < 0))).astype(dt)
         If = 1 - Ic
         Hff = If[:, :, None] * If[:, None, :]
@@ -83,12 +110,16 @@ def pnqp(H, q, lower, upper, x_init=None, n_iter=20, per_problem=False):
         else:
             dx = -np.linalg.solve(H_, g_[..., None])[..., 0]
         J = np.linalg.norm(dx, axis=1) >= 1e-4
+        if margins is not None:
+            _note(margins, "pnqp", np.abs(np.linalg.norm(dx, axis=1) - 1e-4) / 1e-4)
         if J.sum() == 0:
             return x, H_, If, i
         alpha = np.ones(B, dt)
         max_armijo = GAMMA
         count = 0
         while max_armijo <= GAMMA and count < 10:
+            if margins is not None:
+                _note(margins, "pnqp", bound_gap(x + alpha[:, None] * dx))
             maybe_x = eclamp(x + alpha[:, None] * dx, lower, upper)
             armijos = np.full(B, GAMMA + 1e-6, dt)
             with np.errstate(divide="ignore", invalid="ignore"):
@@ -96,6 +127,8 @@ def pnqp(H, q, lower, upper, x_init=None, n_iter=20, per_problem=False):
                 den = np.einsum("bi,bi->b", g, x - maybe_x)
                 armijos[J] = (num / den)[J]
             I = armijos <= GAMMA
+            if margins is not None:
+                _note(margins, "pnqp", np.where(J, np.abs(armijos - GAMMA), np.inf))
             alpha[I] *= dt.type(0.1)
             max_armijo = np.max(armijos)
             count += 1
@@ -104,7 +137,7 @@ def pnqp(H, q, lower, upper, x_init=None, n_iter=20, per_problem=False):
 
 
 def lqr_backward(C, c_back, F, n, m, u=None, u_lower=None, u_upper=None, u_zero_I=None,
-                 m_solver="pinv", per_problem=False):
+                 m_solver="pinv", per_problem=False, margins=None):
     """Backward Riccati sweep in delta space (f_back=None), lqr_step_explicit.py:54-162.
 
     m_solver: 'pinv'  -> per-sample pinverse for m>1 (lqr_step_explicit.py:90-96)
@@ -167,7 +200,8 @@ def lqr_backward(C, c_back, F, n, m, u=None, u_lower=None, u_upper=None, u_zero_
             hi = u_upper if np.ndim(u_upper) == 0 else u_upper[t]
             lb = lo - u[t]
             ub = hi - u[t]
-            kt, Hf, If, it = pnqp(Quu, qu, lb, ub, x_init=prev_kt, n_iter=20, per_problem=per_problem)
+            kt, Hf, If, it = pnqp(Quu, qu, lb, ub, x_init=prev_kt, n_iter=20, per_problem=per_problem,
+                                  margins=margins)
             n_qp += 1 + (int(np.max(it)) if per_problem else it)
             prev_kt = kt
             Qux_ = Qux.copy()
@@ -220,11 +254,19 @@ def quirk_du_norm(u, new_u):
 
 
 def lqr_forward(x_init, C, c, x, u, K, k, dyn, u_lower=None, u_upper=None, u_zero_I=None,
-                linesearch_decay=0.2, max_linesearch_iter=10):
+                linesearch_decay=0.2, max_linesearch_iter=10, margins=None, force_alpha=None):
     """Rollout with batched backtracking line search, lqr_step_explicit.py:166-263.
 
     dyn: callable true dynamics, or ('lin', F, f) for a LinDx.
     Returns new_x, new_u, costs, full_du_norm, alpha_du_norm, mean_alphas, alphas.
+    margins (dict): per problem, the smallest relative distance of an accept
+    test it took (|cost_p - old| / max(1, |old|), key 'linesearch') and of a
+    control it clamped or kept from a bound (key 'clamp').
+    force_alpha [B] (test use): after the line search has made (and recorded)
+    its own decisions, return instead the rollout at these step sizes — the
+    trajectory the search returns when it settles on them — so a test can
+    replay another implementation's decisions and compare arithmetic alone.
+    The returned alphas stay this search's own choices.
     """
     T, B, n = x.shape
     dt = x.dtype
@@ -232,6 +274,7 @@ def lqr_forward(x_init, C, c, x, u, K, k, dyn, u_lower=None, u_upper=None, u_zer
     alphas = np.ones(B, dt)
     current_cost = None
     full_du_norm = None
+    live = np.ones(B, bool)                              # problems still deciding (the rest repeat their pass)
     i = 0
     while (current_cost is None or np.any(current_cost > old_cost)) and i < max_linesearch_iter:
         new_x = [x_init]
@@ -244,6 +287,9 @@ def lqr_forward(x_init, C, c, x, u, K, k, dyn, u_lower=None, u_upper=None, u_zer
             if u_lower is not None:
                 lo = u_lower if np.ndim(u_lower) == 0 else u_lower[t]
                 hi = u_upper if np.ndim(u_upper) == 0 else u_upper[t]
+                if margins is not None:
+                    gap = np.minimum(np.abs(nut - lo), np.abs(nut - hi)) / np.maximum(1.0, np.abs(nut))
+                    _note(margins, "clamp", np.where(live, np.min(gap, axis=1), np.inf))
                 nut = eclamp(nut, lo, hi)
             new_u.append(nut)
             if t < T - 1:
@@ -258,10 +304,45 @@ def lqr_forward(x_init, C, c, x, u, K, k, dyn, u_lower=None, u_upper=None, u_zer
                 dx = nxt - x[t + 1]
         new_x, new_u = np.stack(new_x), np.stack(new_u)
         current_cost = quad_cost_terms(C, c, np.concatenate([new_x, new_u], -1)).sum(0)
+        if margins is not None:
+            rel = np.abs(current_cost - old_cost) / np.maximum(1.0, np.abs(old_cost))
+            last = i == max_linesearch_iter - 1                  # the last pass is accepted regardless
+            _note(margins, "linesearch", np.where(live & (not last), rel, np.inf))
+            live = live & (current_cost > old_cost)
         if full_du_norm is None:
             full_du_norm = quirk_du_norm(u, new_u)
         alphas[current_cost > old_cost] *= dt.type(linesearch_decay)
         i += 1
     alphas[current_cost > old_cost] /= dt.type(linesearch_decay)
+    if force_alpha is not None:
+        new_x, new_u = rollout_at(x_init, x, u, K, k, dyn, np.asarray(force_alpha, dt), u_lower, u_upper, u_zero_I)
+        current_cost = quad_cost_terms(C, c, np.concatenate([new_x, new_u], -1)).sum(0)
     alpha_du_norm = quirk_du_norm(u, new_u)
     return new_x, new_u, current_cost, full_du_norm, alpha_du_norm, np.mean(alphas), alphas
+
+
+def rollout_at(x_init, x, u, K, k, dyn, alphas, u_lower=None, u_upper=None, u_zero_I=None):
+    """One pass of lqr_forward's rollout at per-problem step sizes alphas [B]."""
+    T = x.shape[0]
+    new_x, new_u = [x_init], []
+    dx = np.zeros_like(x_init)
+    for t in range(T):
+        nut = bmv(K[t], dx) + u[t] + alphas[:, None] * k[t]
+        if u_zero_I is not None:
+            nut[u_zero_I[t]] = 0.
+        if u_lower is not None:
+            lo = u_lower if np.ndim(u_lower) == 0 else u_lower[t]
+            hi = u_upper if np.ndim(u_upper) == 0 else u_upper[t]
+            nut = eclamp(nut, lo, hi)
+        new_u.append(nut)
+        if t < T - 1:
+            if isinstance(dyn, tuple):
+                _, F, f = dyn
+                nxt = bmv(F[t], np.concatenate([new_x[t], nut], 1))
+                if f is not None:
+                    nxt = nxt + f[t]
+            else:
+                nxt = dyn(new_x[t], nut)
+            new_x.append(nxt)
+            dx = nxt - x[t + 1]
+    return np.stack(new_x), np.stack(new_u)

@@ -24,11 +24,23 @@ def linearize(model, x, u, params=None):
 
 def mpc_forward(model, x_init, C, c, T, u_init=None, u_lower=None, u_upper=None, lqr_iter=10,
                 eps=1e-7, linesearch_decay=0.2, max_linesearch_iter=10, not_improved_lim=5,
-                best_cost_eps=1e-4, params=None, per_problem=False, m_solver="pinv", trace=None):
+                best_cost_eps=1e-4, params=None, per_problem=False, m_solver="pinv", trace=None, margins=None,
+                force=None):
     """Returns (x [T,B,n], u [T,B,m], costs [B], info).
 
     `model` is one of oracle.models.MODELS, or ('lin', F, f) for a LinDx.
     C/c must already be materialised [T,B,d,d] / [T,B,d].
+    margins (dict): per problem, the smallest relative distance of each kind of
+    discrete decision of the solve from its threshold (keys 'linesearch',
+    'clamp', 'pnqp' from lqr.lqr_forward / lqr.pnqp, 'best' for the best-iterate
+    test cost <= best + best_cost_eps, 'stop' for the batch-wide eps test);
+    margins['min'] is their minimum.  A problem with a clear margin everywhere
+    follows the same decision path in fp32 as in this fp64 restatement.
+    force (test use): force(i) -> (alphas [B], take [B] bool) of iteration i as
+    another implementation decided them; the loop then follows those decisions
+    (the trajectory at those step sizes, those best-iterate updates) while the
+    trace still records its own (trace entries 'alpha_free', 'take_free' and the
+    iteration's decision margins 'ls_margin', 'best_margin').
     """
     B, n = x_init.shape
     d = C.shape[-1]
@@ -46,6 +58,8 @@ def mpc_forward(model, x_init, C, c, T, u_init=None, u_lower=None, u_upper=None,
     n_not_improved = 0
     n_iters = 0
     for i in range(lqr_iter):                                     # mpc_explicit.py:246
+        fa, ft = force(i) if force is not None else (None, None)
+        it_m = {} if (margins is not None or trace is not None) else None
         x = lqr.get_traj(T, u, x_init, dyn)
         if isinstance(model, tuple):
             F, f = model[1], model[2]
@@ -53,27 +67,44 @@ def mpc_forward(model, x_init, C, c, T, u_init=None, u_lower=None, u_upper=None,
             F, f = linearize(model, x, u, params)
         cb = lqr.c_back(C, c, x, u)
         K, k, nqp = lqr.lqr_backward(C, cb, F, n, m, u=u, u_lower=u_lower, u_upper=u_upper,
-                                     m_solver=m_solver, per_problem=per_problem)
-        x, u, costs, full_du_norm, _, mean_alpha, _ = lqr.lqr_forward(
+                                     m_solver=m_solver, per_problem=per_problem, margins=it_m)
+        x, u, costs, full_du_norm, _, mean_alpha, alphas = lqr.lqr_forward(
             x_init, C, c, x, u, K, k, dyn, u_lower=u_lower, u_upper=u_upper,
-            linesearch_decay=linesearch_decay, max_linesearch_iter=max_linesearch_iter)
+            linesearch_decay=linesearch_decay, max_linesearch_iter=max_linesearch_iter, margins=it_m,
+            force_alpha=fa)
         n_iters += 1
         n_not_improved += 1
+        take_free = np.ones(B, bool)
         if best is None:                                          # mpc_explicit.py:269-283
             best = dict(x=x.copy(), u=u.copy(), costs=costs.copy(), du=full_du_norm.copy())
         else:
+            take_free = costs <= best["costs"] + best_cost_eps
+            if it_m is not None:
+                lqr._note(it_m, "best", np.abs(costs - (best["costs"] + best_cost_eps))
+                          / np.maximum(1.0, np.abs(best["costs"])))
+            take = take_free if ft is None else np.asarray(ft, bool)
             for j in range(B):
-                if costs[j] <= best["costs"][j] + best_cost_eps:
+                if take[j]:
                     n_not_improved = 0
                     best["x"][:, j] = x[:, j]
                     best["u"][:, j] = u[:, j]
                     best["costs"][j] = costs[j]
                     best["du"][j] = full_du_norm[j]
+        if it_m is not None and margins is not None:
+            for k_, v in it_m.items():
+                lqr._note(margins, k_, v)
         if trace is not None:
+            inf = np.full(B, np.inf)
             trace.append(dict(x=x.copy(), u=u.copy(), costs=costs.copy(), du=full_du_norm.copy(),
-                              mean_alpha=mean_alpha, nqp=nqp))
+                              mean_alpha=mean_alpha, nqp=nqp, alpha_free=alphas.copy(), take_free=take_free,
+                              ls_margin=it_m.get("linesearch", inf), best_margin=it_m.get("best", inf),
+                              pnqp_margin=it_m.get("pnqp", inf), clamp_margin=it_m.get("clamp", inf)))
+        if margins is not None and eps > 0:                       # batch-wide: every problem
+            lqr._note(margins, "stop", np.full(B, abs(max(full_du_norm) - eps) / eps))
         if max(full_du_norm) < eps or n_not_improved > not_improved_lim:   # mpc_explicit.py:297-299
             break
+    if margins is not None:
+        margins["min"] = np.min(np.stack([v for k_, v in margins.items() if k_ != "min"] or [np.full(B, np.inf)]), 0)
     info = dict(n_iters=n_iters, full_du_norm=best["du"],
                 converged=bool(max(best["du"]) <= eps))
     return best["x"], best["u"], best["costs"], info

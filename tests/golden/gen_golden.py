@@ -648,12 +648,81 @@ def generic_one(dt):
     save(f"generic_{tname(dt)}", **out)
 
 
+# --------------------------------------------------------------------------
+# K. API options: delta_u on LQRStep, u_zero_I on both MPCs and the implicit step
+# --------------------------------------------------------------------------
+def case_api():
+    print("K. api options")
+    for dt in (torch.float64, torch.float32):
+        out = {}
+        with default_dtype(dt), contextlib.redirect_stdout(io.StringIO()):
+            # ---- LQRStep(delta_u) (lqr_step_explicit.py:132-135, 205-213), the lqrstep 'box' setup
+            dx = model("cartpole")
+            T, B = 25, 16
+            rng = np.random.RandomState(11)
+            x0 = xinit_for("cartpole", B, rng)
+            u = rng.uniform(-2, 2, (T, B, 1))
+            X0, U = torch.tensor(x0, dtype=dt), torch.tensor(u, dtype=dt)
+            Q, P = true_cost(dx, T, B, dt)
+            mpc_ = R.mpc_explicit.MPC(5, 1, T, lqr_iter=1)
+            with torch.no_grad():
+                X = R.util.get_traj(T, U, x_init=X0, dynamics=dx)
+                F, f = mpc_.linearize_dynamics(X, U, dx, diff=False)
+                step = R.lqr_step_explicit.LQRStep(
+                    5, 1, T, u_lower=-5.0, u_upper=5.0, delta_u=0.5, true_cost=R.mpc_explicit.QuadCost(Q, P),
+                    true_dynamics=dx, current_x=X, current_u=U, linesearch_decay=0.5, max_linesearch_iter=2)
+                nx, nu, nqp, costs, du, malpha = step(X0, Q, P, F, f, None)
+            out.update(dlt_x0=x0, dlt_u=u, dlt_x=np_(X), dlt_F=np_(F), dlt_f=np_(f), dlt_nx=np_(nx),
+                       dlt_nu=np_(nu), dlt_costs=np_(costs), dlt_malpha=np_(malpha))
+            # ---- MPC(u_zero_I): cartpole unconstrained / +-10, rocket (m = 3) unconstrained
+            for tag, mname, T, B, it, bounds in (("zi_cart", "cartpole", 10, 8, 5, None),
+                                                 ("zi_cartbox", "cartpole", 10, 8, 5, (-10.0, 10.0)),
+                                                 ("zi_rock", "rocket", 10, 4, 3, None)):
+                dxm = model(mname)
+                rng = np.random.RandomState(7)
+                x0 = xinit_for(mname, B, rng)
+                zI = rng.uniform(size=(T, B, dxm.n_ctrl)) < 0.25
+                Q, P = true_cost(dxm, T, B, dt)
+                kw = {} if bounds is None else dict(u_lower=bounds[0], u_upper=bounds[1])
+                decay, mls = (0.5, 2) if mname == "cartpole" else (0.2, 5)
+                m = R.mpc_explicit.MPC(dxm.n_state, dxm.n_ctrl, T, lqr_iter=it, eps=0.0, not_improved_lim=10 ** 9,
+                                       linesearch_decay=decay, max_linesearch_iter=mls, exit_unconverged=False,
+                                       detach_unconverged=False, verbose=-1, u_zero_I=torch.tensor(zI),
+                                       grad_method=R.mpc_explicit.GradMethods.ANALYTIC, **kw)
+                with torch.no_grad():
+                    x, uu, costs = m(torch.tensor(x0, dtype=dt), R.mpc_explicit.QuadCost(Q, P), dxm)
+                out.update({f"{tag}_x0": x0, f"{tag}_zI": zI, f"{tag}_x": np_(x), f"{tag}_u": np_(uu),
+                            f"{tag}_costs": np_(costs)})
+            # ---- the DiLQR no-op step with u_zero_I (its Riccati gains feed the implicit backward)
+            mname, T, B = "cartpole", 10, 4
+            dxm = model(mname)
+            rng = np.random.RandomState(9)
+            x0 = xinit_for(mname, B, rng)
+            u = rng.uniform(-1, 1, (T, B, 1))
+            zI = rng.uniform(size=(T, B, 1)) < 0.25
+            Q, P = true_cost(dxm, T, B, dt)
+            wx, wu = rng.normal(size=(T, B, 5)), rng.normal(size=(T, B, 1))
+            X = R.util.get_traj(T, torch.tensor(u, dtype=dt), x_init=torch.tensor(x0, dtype=dt), dynamics=dxm)
+            theta = dxm.params.detach().clone().to(dt).requires_grad_(True)
+            Qg, Pg = Q.clone().requires_grad_(True), P.clone().requires_grad_(True)
+            mm = R.mpc_explicit.MPC(5, 1, T, grad_method=R.mpc_explicit.GradMethods.ANALYTIC)
+            F, f = mm.linearize_dynamics(X, torch.tensor(u, dtype=dt), dxm, diff=True)
+            step = R.lqr_step_explicit.LQRStep(5, 1, T, u_zero_I=torch.tensor(zI), true_cost=R.mpc_explicit.QuadCost(
+                Qg, Pg), true_dynamics=dxm, current_x=X.detach(), current_u=torch.tensor(u, dtype=dt),
+                back_eps=mm.back_eps, no_op_forward=True)
+            x2, u2 = step(torch.tensor(x0, dtype=dt), Qg, Pg, F.detach(), f.detach(), theta)
+            ((x2 * torch.tensor(wx, dtype=dt)).sum() + (u2 * torch.tensor(wu, dtype=dt)).sum()).backward()
+            out.update(zim_x0=x0, zim_u=u, zim_x=np_(X), zim_zI=zI, zim_wx=wx, zim_wu=wu, zim_dQ=np_(Qg.grad),
+                       zim_dP=np_(Pg.grad), zim_dtheta=np_(theta.grad))
+        save(f"api_{tname(dt)}", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["models", "riccati", "pnqp", "lqrstep", "mpc", "adjoint", "implicit",
-                             "datasets", "il", "generic"]
+                             "datasets", "il", "generic", "api"]
     table = {"models": case_models, "riccati": case_riccati, "pnqp": case_pnqp,
              "lqrstep": case_lqrstep, "mpc": case_mpc, "adjoint": case_classic_adjoint,
              "implicit": case_implicit, "datasets": case_datasets, "il": case_il,
-             "generic": case_generic}
+             "generic": case_generic, "api": case_api}
     for w in which:
         table[w]()

@@ -44,6 +44,18 @@ extern "C" void MODEL##_f_theta(const float* th, const float* x, const float* u,
 }
 WRAP(Pendulum, 4, 3, 1, 3)
 WRAP(Cartpole, 6, 5, 1, 4)
+// get_matrices' second-order pieces (the caller zero-fills, as the kernel does)
+#define WRAPM(MODEL, N, M)                                                                     \
+extern "C" void MODEL##_matrices(const float* th, const float* x, const float* u, float* Dp,   \
+                                 float* Dx, float* Du, float* xth, float* xx) {                \
+  float x_[N], u_[M];                                                                          \
+  for (int i = 0; i < N; ++i) x_[i] = x[i];                                                    \
+  for (int i = 0; i < M; ++i) u_[i] = u[i];                                                    \
+  dilqr::gen::MODEL##D2::matrices(th, x_, u_, Dp, Dx, Du, xth, xx);                             \
+}
+WRAPM(Pendulum, 3, 1)
+WRAPM(Cartpole, 5, 1)
+WRAPM(Rocket, 13, 3)
 // rocket: per-lane pieces, assembled over all lanes
 extern "C" void Rocket_pieces(const float* th, const float* x, const float* u, const float* lam, float* mcol,
                               float* mp, float* xx, float* xth) {
@@ -135,3 +147,30 @@ def test_generated_rocket_pieces(shim, golden):
         assert np.abs(mp - ref_Mp).max() / scale(ref_Mp) < 2e-4, b
         assert np.abs(xxr - xx[b]).max() / scale(xx[b]) < 2e-4, b
         assert np.abs(xth - fth[b]).max() / scale(fth[b]) < 2e-4, b
+
+
+@pytest.mark.parametrize("name", ["pendulum", "cartpole", "rocket"])
+def test_generated_get_matrices_vs_reference(shim, golden, name):
+    """matrices() (the device half of env_dx get_matrices, cartpole.py:105-716,
+    pendulum.py:152-382, rocket.py:258-261 + 541-820) against the reference's
+    own get_matrices outputs (golden 'gm'): D_grad_params, D_grad_x, D_grad_u,
+    x_grad_theta, x_grad_xtm1 (the Jacobian D and x_grad_utm1 = D[:, n:] come
+    from the closed-form Jacobian kernel, pinned elsewhere)."""
+    g = golden("models_f64")
+    cls = {"pendulum": om.Pendulum, "cartpole": om.Cartpole, "rocket": om.Rocket}[name]
+    n, m, p = cls.n_state, cls.n_ctrl, cls.n_params
+    d = n + m
+    X = g[f"{name}_x"][:16]
+    U = g[f"{name}_u"][:16]
+    th = np.array(cls.default_params, np.float32)
+    fn = getattr(shim, name.capitalize() + "_matrices")
+    scale = lambda a: max(1.0, np.abs(a).max())  # noqa: E731
+    for b in range(X.shape[0]):
+        outs = [np.zeros(k, np.float32) for k in (n * d * p, n * d * n, n * d * m, n * p, n * n)]
+        fn(*[a.ctypes.data_as(ctypes.c_void_p) for a in (th, X[b].astype(np.float32), U[b].astype(np.float32),
+                                                          *outs)])
+        Dp, Dx, Du, xth, xx = (o.reshape(sh) for o, sh in zip(outs, ((n, d, p), (n, d, n), (n, d, m), (n, p),
+                                                                     (n, n))))
+        for got, key in ((Dp, "D_params"), (Dx, "D_x"), (Du, "D_u"), (xth, "x_theta"), (xx, "x_xtm1")):
+            ref = g[f"{name}_gm_{key}"][b]
+            assert np.abs(got - ref).max() / scale(ref) < 2e-4, (name, key, b, np.abs(got - ref).max())

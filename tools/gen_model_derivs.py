@@ -99,6 +99,22 @@ def unpack_lines(xs, us, ps, lam=None):
     return s
 
 
+def emit_ptr(name, sig, outputs, unpack):
+    """A function writing the nonzero entries `outputs` [(lvalue, expr)] through
+    pointers (get_matrices; the caller zero-fills the rest), CSE'd."""
+    nz = [(lv, e) for lv, e in outputs if e != 0]
+    repl, red = sp.cse([e for _, e in nz], symbols=sp.numbered_symbols("s"), optimizations="basic")
+    lines = [f"  static DEV void {name}({sig}) {{", unpack]
+    lines += [f"    const float {v} = {P.doprint(e)};" for v, e in repl]
+    lines += [f"    {lv} = {P.doprint(e)};" for (lv, _), e in zip(nz, red)]
+    lines.append("  }")
+    return _f32_calls("\n".join(lines))
+
+
+MAT_SIG = ("float* __restrict__ Dp, float* __restrict__ Dx, float* __restrict__ Du, "
+           "float* __restrict__ xth, float* __restrict__ xx")
+
+
 def model_block(M, cls_name):
     n, m, p = M.n, M.m, M.p
     d = n + m
@@ -125,8 +141,28 @@ def model_block(M, cls_name):
         head, rest = body.split("{", 1)
         return head + "{\n" + unpack + (unpack_l if with_lam else "") + rest
 
+    # get_matrices (cartpole.py:105-716, pendulum.py:152-382): D_grad_params
+    # [n][d][p] (with the reference's overrides), D_grad_x [n][d][n], D_grad_u
+    # [n][d][m], x_grad_theta [n][p], x_grad_xtm1 [n][n] = D[:, :n] (cartpole:
+    # its [0][0] written 0, cartpole.py:666)
+    mats = []
+    for i in range(n):
+        for j in range(d):
+            for k in range(p):
+                mats.append((f"Dp[{(i * d + j) * p + k}]", Dp[i][j][k]))
+            for k in range(n):
+                mats.append((f"Dx[{(i * d + j) * n + k}]", sp.diff(D[i, j], xs[k])))
+            for k in range(m):
+                mats.append((f"Du[{(i * d + j) * m + k}]", sp.diff(D[i, j], us[k])))
+    for i in range(n):
+        for k in range(p):
+            mats.append((f"xth[{i * p + k}]", ft[i][k]))
+        for k in range(n):
+            zero = M.xx00_zero and i == 0 and k == 0
+            mats.append((f"xx[{i * n + k}]", sp.Integer(0) if zero else D[i, k]))
     parts = [f"struct {cls_name} {{",
              f"  static constexpr int N = {n}, M = {m}, P = {p}, D = {d};",
+             emit_ptr("matrices", sig + ", " + MAT_SIG, mats, unpack),
              fn("lag_hess", f", const float (&lam)[{n}]",
                 [(f"Mo[{j}][{k}]", Mh[j][k]) for j in range(d) for k in range(d)], f"float (&Mo)[{d}][{d}]", True),
              fn("lag_dparam", f", const float (&lam)[{n}]",
@@ -179,8 +215,15 @@ def rocket_block():
     sig = f"const float* __restrict__ th, const float (&x)[{n}], const float (&u)[{m}]"
     sig_l = sig + f", const float (&lam)[{n}]"
     up, upl = unpack_lines(xs, us, ps), unpack_lines(xs, us, ps, lam)
+    # get_matrices (rocket.py:258-261 with the build_batched_* tables)
+    mats = [(f"Dp[{(i * d + j) * p + k}]", e) for (i, j, k), e in sorted(Dp.items())]
+    mats += [(f"Dx[{(i * d + j) * n + k}]", e) for (i, j, k), e in sorted(Dx.items())]
+    mats += [(f"Du[{(i * d + j) * m + k}]", e) for (i, j, k), e in sorted(Du.items())]
+    mats += [(f"xth[{i * p + k}]", sp.diff(f[i], ps[k])) for i in range(n) for k in range(p)]
+    mats += [(f"xx[{i * n + k}]", e) for (i, k), e in sorted(xx.items())]
     parts = ["struct RocketD2 {",
              f"  static constexpr int N = {n}, M = {m}, P = {p}, D = {d};",
+             emit_ptr("matrices", sig + ", " + MAT_SIG, mats, up),
              emit_switch("mcol", sig_l, "r", d, mcol, upl),
              emit_switch("mp_row", sig_l, "j", p, mp, upl),
              emit_switch("xx_row", sig, "r", n, xxr, up),

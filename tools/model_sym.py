@@ -24,6 +24,7 @@ def symbols(n, m, p):
 # ------------------------------------------------------------------ pendulum
 class Pendulum:
     n, m, p = 3, 1, 3
+    xx00_zero = False         # x_grad_xtm1 is D[:, :n] as computed (pendulum.py:152-382)
     dt = 0.05
 
     @classmethod
@@ -44,6 +45,7 @@ class Pendulum:
 # ------------------------------------------------------------------ cartpole
 class Cartpole:
     n, m, p = 5, 1, 4
+    xx00_zero = True          # the reference writes x_grad_xtm1[0,0] = 0 (cartpole.py:666)
     dt = 0.05
 
     @classmethod
