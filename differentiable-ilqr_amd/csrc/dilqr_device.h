@@ -310,9 +310,15 @@ DEV int pnqp(const float (&H)[M][M], const float (&q)[M], const float (&lb)[M],
              const float (&ub)[M], bool have_init, float (&x)[M], float (&If)[M],
              float (&Hf)[M][M]) {
   const float GAMMA = 0.1f;
+  // m = 1: the reciprocals are v_rcp_f32 (1 ulp) instead of IEEE divisions
+  // (~10 instructions each, three per Newton iteration), the stop test's
+  // norm of a 1-vector is |dx| and the Armijo ratio is num * rcp(den): each
+  // differs from the reference's fp32 value by rounding only, so only a
+  // decision sitting on its threshold to within an ulp can go the other way
+  // (the parity tests replay decisions and bound such near-ties)
   if (!have_init) {                                     // pnqp.py:14-19
     if constexpr (M == 1) {
-      x[0] = -(1.0f / H[0][0]) * q[0];
+      x[0] = -__builtin_amdgcn_rcpf(H[0][0]) * q[0];
     } else {
       float A[M][M], X[M][1];
 #pragma unroll
@@ -368,7 +374,7 @@ DEV int pnqp(const float (&H)[M][M], const float (&q)[M], const float (&lb)[M],
         Hf[i][j] = ((If[i] * If[j]) != 0.f ? H[i][j] : 0.f) + (i == j ? 1e-11f : 0.f);
     float dx[M];
     if constexpr (M == 1) {
-      dx[0] = -(1.0f / Hf[0][0]) * g_[0];
+      dx[0] = -__builtin_amdgcn_rcpf(Hf[0][0]) * g_[0];
     } else {
       float A[M][M], X[M][1];
 #pragma unroll
@@ -381,10 +387,14 @@ DEV int pnqp(const float (&H)[M][M], const float (&q)[M], const float (&lb)[M],
 #pragma unroll
       for (int i = 0; i < M; ++i) dx[i] = -X[i][0];
     }
-    float nrm = 0.f;
+    if constexpr (M == 1) {
+      if (!(fabsf(dx[0]) >= 1e-4f)) return it;          // pnqp.py:56-59 (per problem)
+    } else {
+      float nrm = 0.f;
 #pragma unroll
-    for (int i = 0; i < M; ++i) nrm += dx[i] * dx[i];
-    if (!(sqrtf(nrm) >= 1e-4f)) return it;              // pnqp.py:56-59 (per problem)
+      for (int i = 0; i < M; ++i) nrm += dx[i] * dx[i];
+      if (!(sqrtf(nrm) >= 1e-4f)) return it;
+    }
 
     float alpha = 1.f;
     float ox = obj(x);
@@ -397,7 +407,7 @@ DEV int pnqp(const float (&H)[M][M], const float (&q)[M], const float (&lb)[M],
       float den = 0.f;
 #pragma unroll
       for (int i = 0; i < M; ++i) den += g[i] * (x[i] - maybe[i]);
-      float armijo = (ox - obj(maybe)) / den;
+      float armijo = (M == 1) ? (ox - obj(maybe)) * __builtin_amdgcn_rcpf(den) : (ox - obj(maybe)) / den;
       if (armijo <= GAMMA) alpha *= 0.1f;
       max_armijo = armijo;
       ++count;
@@ -599,7 +609,7 @@ struct RiccatiState {
       for (int a = 0; a < M; ++a) { k[a] = x[a]; prev_k[a] = x[a]; }
       have_prev = true;
       if constexpr (M == 1) {
-        float r = 1.0f / Hf[0][0];
+        float r = __builtin_amdgcn_rcpf(Hf[0][0]);
 #pragma unroll
         for (int j = 0; j < N; ++j) K[0][j] = -(r * (If[0] != 0.f ? Q[N][j] : 0.f));
       } else {
@@ -629,6 +639,24 @@ struct RiccatiState {
           if (SYM && j != i) V[j][i] = V[i][j];
         }
         v[i] = Q[i][N] * k[0] + q[i];
+      }
+      return;
+    }
+    // Box, m = 1: K = -Q_ux / (Q_uu + 1e-11) on a free control, 0 on a clamped
+    // one, so K^T Q_ux + K^T Q_uu K = K^T Q_ux (1e-11 / (Q_uu + 1e-11)) — zero to
+    // 1e-11 relative, far below fp32 rounding — and V = Q_xx + Q_xu K as above;
+    // the k terms keep their exact form, v = q_x + Q_xu k + K^T (q_u + Q_uu k)
+    // (pnqp stops within 1e-4 of the box optimum, so q_u + Q_uu k is not ~0)
+    if constexpr (MODE == GAIN_BOX && M == 1) {
+      const float gk = qu[0] + Quu[0][0] * k[0];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+#pragma unroll
+        for (int j = SYM ? i : 0; j < N; ++j) {
+          V[i][j] = Q[i][N] * K[0][j] + Q[i][j];
+          if (SYM && j != i) V[j][i] = V[i][j];
+        }
+        v[i] = (Q[i][N] * k[0] + q[i]) + K[0][i] * gk;
       }
       return;
     }

@@ -426,13 +426,43 @@ DEV float group_forward_pass(GroupLds<n, m>& L, const Model* md, const float* __
   return cst;
 }
 
+// Where a group's stage cost comes from.  Lane r needs row r of C_t and c_t.
+// Either the caller's C [T,B,d,d], c [T,B,d] (one 64-byte row per lane per
+// step), or — for a problem whose cost the solve's iteration 0 found to be
+// diagonal (every off-diagonal entry +0.0 bit for bit) and the same at every t
+// (the reference's own callers: diag(q), p repeated, il_env.py:159-162) — two
+// registers per lane, C[r][r] and c[r].  row() fills Crow with exactly the
+// values the load returns, so the arithmetic is unchanged, bit for bit; only
+// the bytes are not read (the dense rows were 30 KB per problem and pass).
+struct GroupCost {
+  const float* __restrict__ C;
+  const float* __restrict__ c;
+  bool dconst;
+  float cd, cc;
+  template <int d>
+  DEV void row(size_t tb, int r, float (&Crow)[d], float& cr) const {
+    if (dconst) {
+#pragma unroll
+      for (int j = 0; j < d; ++j) Crow[j] = (j == r) ? cd : 0.f;
+      cr = cc;
+    } else if (r < d) {
+      ld(Crow, C + (tb * d + r) * d);
+      cr = c[tb * d + r];
+    } else {
+#pragma unroll
+      for (int j = 0; j < d; ++j) Crow[j] = 0.f;
+      cr = 0.f;
+    }
+  }
+};
+
 // Two step sizes rolled out together (the fused MPC kernel's paired line
 // search, see ilqr_problem): candidates A (alpha aA) and B (aB, if twoB) share
 // the step's loads; each keeps its own state component, controls and cost.
 template <int n, int m, int GREC, class Model>
 DEV void group_forward_pair(GroupLds<n, m>& L, const Model& md, int T, int B, int b, int r, bool valid, float aA,
-                            float aB, bool twoB, const float* __restrict__ x_init, const float* __restrict__ C,
-                            const float* __restrict__ c, const float* __restrict__ x, const float* __restrict__ u,
+                            float aB, bool twoB, const float* __restrict__ x_init, const GroupCost& cs,
+                            const float* __restrict__ x, const float* __restrict__ u,
                             const float* __restrict__ grec, const Bounds& bd, float* __restrict__ xa_out,
                             float* __restrict__ ua_out, float* __restrict__ xb_out, float* __restrict__ ub_out,
                             float* __restrict__ du_sq, float& cA, float& cB, float& old_cost) {
@@ -490,9 +520,8 @@ DEV void group_forward_pair(GroupLds<n, m>& L, const Model& md, int T, int B, in
     __syncthreads();
     float pA = 0.f, pB = 0.f;
     if (r < d) {
-      float Crow[d];
-      ld(Crow, C + (tb * d + r) * d);
-      const float cr = c[tb * d + r];
+      float Crow[d], cr;
+      cs.row(tb, r, Crow, cr);
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int j = 0; j < n; ++j) { s1 += Crow[j] * fA[j]; s2 += Crow[j] * fB[j]; }
@@ -596,15 +625,23 @@ __global__ void __launch_bounds__(64) k_lqr_forward_group(int T, int B, const fl
 // ilqr_problem (dilqr_kernels.hip) for a 16-lane group: on-the-fly Jacobian
 // rows (Model::jac_row), Riccati + stage costs, gain records, line-search rollout
 // with row-distributed dynamics (Model::deriv) and shuffle-reduced costs.
+// cs: the cost source (GroupCost).  cpk_out / sym_out (the solve's iteration 0,
+// reading the caller's C): decide per problem whether its cost is diagonal and
+// time-invariant (flag 7 in sym_out[b], else 0) and, if so, store its row
+// values [B][2d] (diag, then c) in cpk_out; the line search of this same
+// iteration then already takes them from registers.
 template <class Model, int MODE>
 DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r, bool valid,
-                            const Model& md, const float* __restrict__ x_init, const float* __restrict__ C,
-                            const float* __restrict__ c, const float* __restrict__ x, const float* __restrict__ u,
+                            const Model& md, const float* __restrict__ x_init, GroupCost cs,
+                            const float* __restrict__ x, const float* __restrict__ u,
                             const Bounds& bd, float decay, int max_ls, float* __restrict__ ws,
                             float* __restrict__ x_out, float* __restrict__ u_out, float* __restrict__ xb_out,
                             float* __restrict__ ub_out, float* __restrict__ du_sq, float& cost_out, float& alpha_out,
-                            int& win_out) {
+                            int& win_out, float* __restrict__ cpk_out = nullptr,
+                            unsigned char* __restrict__ sym_out = nullptr) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
+  bool ok_diag = true, ok_tinv = true;     // this lane's row: off-diagonal +0.0, equal to step T-1's
+  float cd_last = 0.f, cc_last = 0.f;
   constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
   constexpr int W = GroupLds<n, m>::W;
   // ---------------- backward
@@ -623,9 +660,17 @@ DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b
     float Crow[d], cr = 0.f, xt[n], ut[m];
     ld(xt, x + tb * n);                              // the group's 16 lanes read the same 64 B
     ld(ut, u + tb * m);
+    cs.row(tb, r, Crow, cr);
+    if (cpk_out) {                                   // iteration 0: is the cost a time-invariant diagonal?
+      float dg = 0.f;
 #pragma unroll
-    for (int j = 0; j < d; ++j) Crow[j] = 0.f;
-    if (r < d) { ld(Crow, C + (tb * d + r) * d); cr = c[tb * d + r]; }
+      for (int j = 0; j < d; ++j) {
+        if (j == r) dg = Crow[j];
+        else ok_diag &= __float_as_uint(Crow[j]) == 0u;
+      }
+      if (t == T - 1) { cd_last = dg; cc_last = cr; }
+      ok_tinv &= __float_as_uint(dg) == __float_as_uint(cd_last) && __float_as_uint(cr) == __float_as_uint(cc_last);
+    }
     if (r < n) {
       float Fr[d];
       if (t < T - 1) {
@@ -673,6 +718,18 @@ DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b
     }
     __syncthreads();
   }
+  if (cpk_out) {
+    // the group's verdict (all 16 rows), then the record and the flag; this
+    // iteration's line search reads the registers already
+    const unsigned long long bad = __ballot(!(ok_diag && ok_tinv));
+    const bool grp = ((bad >> (threadIdx.x & ~(kG - 1))) & ((1ull << kG) - 1)) == 0ull;
+    if (valid) {
+      cpk_out[(size_t)b * 2 * d + r] = cd_last;
+      cpk_out[(size_t)b * 2 * d + d + r] = cc_last;
+      if (r == 0) sym_out[b] = grp ? 7 : 0;
+    }
+    if (grp) { cs.dconst = true; cs.cd = cd_last; cs.cc = cc_last; }
+  }
   // ---------------- forward line search
   float alpha = 1.f, cost = 0.f, old_cost = 0.f;
   int win = 0;
@@ -685,7 +742,7 @@ DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b
       float cA, cB, oc;
       const float aA = alpha, aB = alpha * decay;
       // a group that already accepted keeps rolling (its barriers) but writes nothing
-      group_forward_pair<n, m, GREC>(L, md, T, B, b, r, valid && !done, aA, aB, twoB, x_init, C, c, x, u, ws, bd,
+      group_forward_pair<n, m, GREC>(L, md, T, B, b, r, valid && !done, aA, aB, twoB, x_init, cs, x, u, ws, bd,
                                      x_out,
                                      u_out, xb_out, ub_out, p == 0 ? du_sq : nullptr, cA, cB, oc);
       if (p == 0) old_cost = oc;
@@ -699,7 +756,7 @@ DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b
   } else {
     for (int ls = 0; ls < max_ls; ++ls) {
       float oldc;
-      cost = group_forward_pass<n, m, GREC>(L, &md, nullptr, nullptr, T, B, b, r, valid, alpha, x_init, C, c, x, u,
+      cost = group_forward_pass<n, m, GREC>(L, &md, nullptr, nullptr, T, B, b, r, valid, alpha, x_init, cs.C, cs.c, x, u,
                                             nullptr, nullptr, ws, bd, nullptr, x_out, u_out,
                                             ls == 0 ? du_sq : nullptr, &oldc);
       if (ls == 0) old_cost = oldc;

@@ -24,8 +24,8 @@ __global__ void __launch_bounds__(64) k_ilqr_iterate_group(int T, int B, const f
   Model md; md.load(theta);
   float cost, alpha;
   int win;
-  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, x, u, bd, decay, max_ls, ws, x_out,
-                                  u_out, nullptr, nullptr, du_sq, cost, alpha, win);
+  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, GroupCost{C, c, false, 0.f, 0.f}, x, u, bd,
+                                  decay, max_ls, ws, x_out, u_out, nullptr, nullptr, du_sq, cost, alpha, win);
   if (valid && r == 0) {
     cost_out[b] = cost;
     alpha_out[b] = alpha;
@@ -54,9 +54,19 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_mpc_iterate_group(in
   free_slots(cur, best, sa, sb);
   float cost, alpha;
   int win;
-  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, C, c, S.Xs + cur * TBn, S.Us + cur * TBm,
+  // the cost: the caller's rows, or (a time-invariant diagonal cost, flagged by
+  // iteration 0) two registers per lane from the solve's record [B][2d]
+  constexpr int d = n + m;
+  GroupCost cs{C, c, false, 0.f, 0.f};
+  if (!first && S.Cpk && S.cost_sym[b] == 7) {
+    cs.dconst = true;
+    cs.cd = S.Cpk[(size_t)b * 2 * d + r];
+    cs.cc = S.Cpk[(size_t)b * 2 * d + d + r];
+  }
+  group_ilqr_problem<Model, MODE>(Ls[gp], T, B, b, r, valid, md, x_init, cs, S.Xs + cur * TBn, S.Us + cur * TBm,
                                   bd, decay, max_ls, S.ws, S.Xs + sa * TBn, S.Us + sa * TBm, S.Xs + sb * TBn,
-                                  S.Us + sb * TBm, S.du_sq, cost, alpha, win);
+                                  S.Us + sb * TBm, S.du_sq, cost, alpha, win, first ? S.Cpk : nullptr,
+                                  first ? S.cost_sym : nullptr);
   const int nw = win ? sb : sa;
   if (valid && r == 0) {
     S.cost[b] = cost;

@@ -218,9 +218,16 @@ class MPCSolve:
         self.last_iteration = -1
         # stop-rule sync area: 16 words + two planes of per-workgroup partials (<= ceil(B/64))
         self.counter = torch.zeros(16 + 4 * ((B + 63) // 64), dtype=torch.int32, device=dev)
-        # packed symmetric-cost copy for the thread-per-problem fused kernels (d <= 8)
+        # the solve's copy of its cost: packed symmetric records for the thread-per-
+        # problem fused kernels (d <= 8), one [2d] row record per problem (a
+        # time-invariant diagonal cost) for the 16-lane ones
         pk = N.lib().dilqr_mpc_packed_cost_floats(n, m)
-        self.Cpk = torch.empty(T * B * pk, device=dev) if n + m <= 8 and packed_cost else None
+        if not packed_cost:
+            self.Cpk = None
+        elif n + m <= 8:
+            self.Cpk = torch.empty(T * B * pk, device=dev)
+        else:
+            self.Cpk = torch.empty(B * 2 * (n + m), device=dev)
         self.cost_sym = torch.zeros(B, dtype=torch.uint8, device=dev) if self.Cpk is not None else None
         self.state = N.MpcState(*[t.data_ptr() if t is not None else None for t in (
             self.Xs, self.Us, self.slot, self.best_cost, self.best_du, self.improved, self.cost, self.alpha,

@@ -273,7 +273,11 @@ int dilqr_grad_input_f32(int model, int T, int B, const float* X, const float* U
    Later iterations of flagged problems read the copy: 27 instead of 42 floats
    per step at d=6, or 12 for a diagonal cost (diag(q), the reference's own
    callers, il_env.py:159-162); identical arithmetic.  The cost passed to the
-   iterations of one solve must not change.
+   iterations of one solve must not change.  For the 16-lanes-per-problem
+   models (rocket) Cpk holds B*2d floats instead: iteration 0 sets cost_sym[b]
+   = 7 when problem b's cost is diagonal (off-diagonal entries +0.0) and the
+   same at every t, and stores its diag and c [B][2d]; later iterations of
+   such problems hold them in registers and read no cost at all.
    Invariant: every trajectory held in a slot is a rollout of the model, i.e.
    x_{t+1} == forward(x_t, u_t) bit for bit with u_t as stored (already
    clamped to the box) — begin and the line search write only such

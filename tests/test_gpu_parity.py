@@ -417,7 +417,9 @@ def test_dataset_cartpole_known_answer(golden):
                           5, float(g["cartpole_linesearch_decay"]), int(g["cartpole_max_linesearch_iter"]))
     got = np.concatenate([cpu(x), cpu(u)], 2).transpose(1, 0, 2)
     print(f"\n[dataset cartpole] max |got - reference| {np.max(np.abs(got - tau)):.2e}")
-    assert np.max(np.abs(got - tau)) < 1e-2
+    # the reference reproduces this dataset bit for bit; the fp32
+    # GPU solve (other summation orders, v_rcp gains) is measured at 9.3e-6
+    assert np.max(np.abs(got - tau)) < 1e-4
 
 
 def test_dataset_pendulum_known_answer(golden):
@@ -433,9 +435,11 @@ def test_dataset_pendulum_known_answer(golden):
     err = np.abs(got - tau).max(axis=(1, 2))
     print(f"\n[dataset pendulum] per-trajectory max err: median {np.median(err):.2e}, 99% {np.quantile(err, .99):.2e}, "
           f"max {err.max():.2e}, within 1e-4: {np.mean(err < 1e-4):.3f}")
-    # the reference reproduces its own dataset only to 7e-4; we
-    # require 99% of trajectories within 1e-2 and all within 5e-2
-    assert np.mean(err < 1e-2) >= 0.99 and err.max() < 5e-2, (np.mean(err < 1e-2), err.max())
+    # the reference reproduces its own dataset only to 7e-4 (500
+    # iterations with eps 1e-3 on saturated controls); measured here: median
+    # 1.2e-6, 91% of trajectories within 1e-4, max 3.7e-4
+    assert np.median(err) < 1e-5 and np.mean(err < 1e-4) >= 0.85 and err.max() < 1e-3, \
+        (np.median(err), np.mean(err < 1e-4), err.max())
 
 
 # ------------------------------------------------------------------ full-size properties
@@ -543,13 +547,13 @@ def test_mpc_end_to_end_gradient(golden):
     mpc = dilqr.MPC(5, 1, T, u_lower=-5.0, u_upper=5.0, lqr_iter=30, eps=1e-6, linesearch_decay=0.5,
                     max_linesearch_iter=2, exit_unconverged=False, detach_unconverged=False)
     x, u, _ = mpc(x0, dilqr.QuadCost(Q, P), dx)
-    assert relerr(cpu(u), g[f"{tag}_u"]) < 1e-3
+    assert relerr(cpu(u), g[f"{tag}_u"]) < 1e-4
     loss = (x * gpu(g[f"{tag}_wx"])).sum() + (u * gpu(g[f"{tag}_wu"])).sum()
     loss.backward()
     print(f"\n[end-to-end] u {relerr(cpu(u), g[f'{tag}_u']):.2e}, dtheta "
           f"{relerr(cpu(dx.params.grad), g[f'{tag}_dtheta']):.2e}, dQ {relerr(cpu(Q.grad), g[f'{tag}_dQ']):.2e}")
-    assert relerr(cpu(dx.params.grad), g[f"{tag}_dtheta"]) < 5e-3
-    assert relerr(cpu(Q.grad), g[f"{tag}_dQ"]) < 5e-3
+    assert relerr(cpu(dx.params.grad), g[f"{tag}_dtheta"]) < 1e-4
+    assert relerr(cpu(Q.grad), g[f"{tag}_dQ"]) < 1e-4
 
 
 def test_implicit_backward_full_size():
@@ -704,10 +708,11 @@ def test_rocket_fused_iteration_equals_unfused(golden):
     x0 = g["rocket_unc_x0"]
     a = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls, fused=True)
     b = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls, fused=False)
-    errs = [relerr(cpu(ta), cpu(tb)) for ta, tb in zip(a, b)]
-    print(f"\n[rocket fused vs unfused] x {errs[0]:.2e} u {errs[1]:.2e} cost {errs[2]:.2e}")
-    for e in errs:
-        assert e < 1e-3
+    # the 16-lane fused iteration (on-the-fly Jacobian rows, the cost in
+    # registers) and the unfused kernels (k_linearize -> F in HBM -> sweep ->
+    # line search) do the same arithmetic: bit for bit
+    for ta, tb in zip(a, b):
+        assert same_bits(ta, tb), relerr(cpu(ta), cpu(tb))
 
 
 def test_rocket_mpc_full_size_batch_independence():
@@ -922,3 +927,38 @@ def test_implicit_backward_u_zero_I_vs_golden(golden):
     errs = (relerr(cpu(theta.grad), g["zim_dtheta"]), relerr(cpu(Q.grad), g["zim_dQ"]), relerr(cpu(P.grad), g["zim_dP"]))
     print(f"\n[u_zero_I implicit] dtheta {errs[0]:.2e} dQ {errs[1]:.2e} dP {errs[2]:.2e}")
     assert max(errs) < 1e-4
+
+
+def test_rocket_register_cost_bit_identical():
+    """The 16-lane MPC kernel holds a time-invariant diagonal cost in two
+    registers per lane (flag 7 from iteration 0) instead of reading the caller's
+    16 x 16 rows every step and pass: the same values, so bit-identical
+    trajectories and costs with and without the solve's cost record, on a batch
+    that mixes flagged problems with a time-varying and a non-diagonal cost."""
+    from dilqr import _native as N
+    from dilqr import ops
+    dx = dilqr_models()["rocket"]()
+    T, B, n, m = 12, 64, 13, 3
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1)
+    c = p.repeat(T, B, 1).clone()
+    C[:, 40:48, 0, 1] += 1e-3                     # not diagonal
+    C[:, 40:48, 1, 0] += 1e-3
+    c[3, 48:56] += 0.01                           # not time-invariant
+    C, c = C.to(DEV).contiguous(), c.to(DEV).contiguous()
+    x0 = gpu(rocket_x0(B, seed=4))
+    theta = ops.theta_of(dx, x0)
+    nb, _ = N.make_bounds(None, None)
+    out = []
+    for packed in (True, False):
+        sv = ops.MPCSolve(T, B, n, m, DEV, packed_cost=packed)
+        sv.begin(dx.model_id, theta, x0)
+        for i in range(4):
+            sv.iterate(dx.model_id, theta, x0, C, c, nb, 0.2, 5, i, 1e-4, 0.0, 10 ** 9)
+        x, u = sv.gather_best()
+        out.append((x, u, sv.best_cost.clone()))
+        if packed:
+            flags = cpu(sv.cost_sym)
+            assert (flags[:40] == 7).all() and (flags[56:] == 7).all() and (flags[40:56] == 0).all()
+    for a, b in zip(*out):
+        assert same_bits(a, b)
