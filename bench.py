@@ -226,8 +226,17 @@ def load_pmc():
 
 def with_pmc(entry, sig):
     """Attach the PMC figures of kernel `sig` (HBM-side bytes -> traffic, issue
-    fractions) to a roofline entry."""
-    k = load_pmc().get(sig)
+    fractions) to a roofline entry.  A tuple of signatures: the launches of one
+    step together (traffic summed, counters per kernel)."""
+    pmc = load_pmc()
+    if isinstance(sig, tuple):
+        ks = [pmc.get(s_) for s_ in sig]
+        if all(ks):
+            entry["traffic"] = sum(k.get("hbm_bytes_per_launch", 0.0) for k in ks)
+            entry["pmc"] = {s_: {f: v for f, v in k.items() if f != "hbm_bytes_per_launch"} for s_, k in zip(sig, ks)}
+            entry["pmc_measured_at"] = PMC_COMMIT[0]
+        return entry
+    k = pmc.get(sig)
     if k:
         entry["traffic"] = k.get("hbm_bytes_per_launch")
         entry["pmc"] = {f: v for f, v in k.items() if f != "hbm_bytes_per_launch"}
@@ -322,7 +331,8 @@ def secondary_configs(dev):
     sv = ops.MPCSolve(T, B, n, m, dev, fixed_iters=10)
     nb, _ = N.make_bounds(None, None)
     val, ms_it = _timed_solves(sv, N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, 10, 2, 1)
-    # the kernel the timed solves run: k_mpc_iterate_group<Rocket> in steady state
+    # the launches the timed solves run per iteration, steady state: the group
+    # sweep (16 lanes per problem) and the line search (one problem per lane)
     it_ms = steady_iteration_ms(ops.MPCSolve(T, B, n, m, dev), N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, dev)
     d = n + m
     it_bytes = 4 * (T * d * d + T * d + n + 2 * T * d + 2) * B                 # 36,540 B/problem, SURVEY §8(d)
@@ -330,10 +340,11 @@ def secondary_configs(dev):
     out["config3_rocket"] = {
         "value": val, "unit": "problem-iters/s", "ms_per_iter": ms_it, "batch": B, "T": T,
         "fused_iteration": with_pmc(
-            {"kernel": "k_mpc_iterate_group<Rocket,UNC> (the timed solves' kernel, steady state)",
+            {"kernel": "k_mpc_sweep_group<Rocket,UNC> + k_mpc_search_lane<Rocket,NONE> (one MPC iteration of "
+                       "the timed solves, steady state)",
              "bound": "hbm", "avg_launch_ms": it_ms, "algorithmic_bytes_per_launch": it_bytes,
              "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
-            "k_mpc_iterate_group<Rocket, 0>"),
+            ("k_mpc_sweep_group<Rocket, 0>", "k_mpc_search_lane<Rocket, 0>")),
         "riccati_sweep": sweep_roofline(n, m, T, B, dev)}
     # rocket implicit backward (16-lane groups) at the solution of the timed solves
     x, u = sv.gather_best()
@@ -425,7 +436,7 @@ def profile_set(name, dev):
     from dilqr import ops
     from dilqr.implicit import implicit_backward
     out = {}
-    if name == "rocket":                          # k_mpc_iterate_group<Rocket,UNC>, config 3
+    if name == "rocket":                          # k_mpc_sweep_group + k_mpc_search_lane<Rocket>, config 3
         T, B = 30, 32768
         dx, x0, C, c = rocket_problems(B, dev)
         theta = ops.theta_of(dx, x0)

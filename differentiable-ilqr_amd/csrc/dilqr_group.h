@@ -622,27 +622,26 @@ __global__ void __launch_bounds__(64) k_lqr_forward_group(int T, int B, const fl
 }
 
 // ---------------------------------------------------------------- fused iteration
-// ilqr_problem (dilqr_kernels.hip) for a 16-lane group: on-the-fly Jacobian
-// rows (Model::jac_row), Riccati + stage costs, gain records, line-search rollout
-// with row-distributed dynamics (Model::deriv) and shuffle-reduced costs.
+// The backward half of ilqr_problem (dilqr_fused.h) for a 16-lane group:
+// on-the-fly Jacobian rows (Model::jac_row), Riccati + the current stage costs;
+// gain records (K_t, k_t, stage cost) go to ws [T,B,GREC].
 // cs: the cost source (GroupCost).  cpk_out / sym_out (the solve's iteration 0,
 // reading the caller's C): decide per problem whether its cost is diagonal and
 // time-invariant (flag 7 in sym_out[b], else 0) and, if so, store its row
-// values [B][2d] (diag, then c) in cpk_out; the line search of this same
-// iteration then already takes them from registers.
+// values [B][2d] (diag, then c) in cpk_out and switch cs to them, so that a line
+// search of this same iteration already takes them from registers.
+template <class Model>
+constexpr int group_grec() { return ((Model::M * Model::N + Model::M + 1) + 3) / 4 * 4; }
+
 template <class Model, int MODE>
-DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r, bool valid,
-                            const Model& md, const float* __restrict__ x_init, GroupCost cs,
-                            const float* __restrict__ x, const float* __restrict__ u,
-                            const Bounds& bd, float decay, int max_ls, float* __restrict__ ws,
-                            float* __restrict__ x_out, float* __restrict__ u_out, float* __restrict__ xb_out,
-                            float* __restrict__ ub_out, float* __restrict__ du_sq, float& cost_out, float& alpha_out,
-                            int& win_out, float* __restrict__ cpk_out = nullptr,
-                            unsigned char* __restrict__ sym_out = nullptr) {
+DEV void group_sweep(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r, bool valid, const Model& md,
+                     GroupCost& cs, const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd,
+                     float* __restrict__ ws, float* __restrict__ cpk_out = nullptr,
+                     unsigned char* __restrict__ sym_out = nullptr) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
   bool ok_diag = true, ok_tinv = true;     // this lane's row: off-diagonal +0.0, equal to step T-1's
   float cd_last = 0.f, cc_last = 0.f;
-  constexpr int GREC = ((m * n + m + 1) + 3) / 4 * 4;
+  constexpr int GREC = group_grec<Model>();
   constexpr int W = GroupLds<n, m>::W;
   // ---------------- backward
   if (r < n) {
@@ -730,6 +729,23 @@ DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b
     }
     if (grp) { cs.dconst = true; cs.cd = cd_last; cs.cc = cc_last; }
   }
+}
+
+// ilqr_problem (dilqr_fused.h) for a 16-lane group: group_sweep, then the
+// line-search rollout with row-distributed dynamics (Model::forward_row) and
+// shuffle-reduced costs.  (The rocket MPC iteration runs its line search one
+// problem per lane instead: dilqr_lane_search.h.)
+template <class Model, int MODE>
+DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r, bool valid,
+                            const Model& md, const float* __restrict__ x_init, GroupCost cs,
+                            const float* __restrict__ x, const float* __restrict__ u,
+                            const Bounds& bd, float decay, int max_ls, float* __restrict__ ws,
+                            float* __restrict__ x_out, float* __restrict__ u_out, float* __restrict__ xb_out,
+                            float* __restrict__ ub_out, float* __restrict__ du_sq, float& cost_out, float& alpha_out,
+                            int& win_out) {
+  constexpr int n = Model::N, m = Model::M;
+  constexpr int GREC = group_grec<Model>();
+  group_sweep<Model, MODE>(L, T, B, b, r, valid, md, cs, x, u, bd, ws);
   // ---------------- forward line search
   float alpha = 1.f, cost = 0.f, old_cost = 0.f;
   int win = 0;
