@@ -240,8 +240,155 @@ DEV void group_riccati_step(GroupLds<n, m>& L, int r, const float (&Crow)[n + m]
   }
 }
 
+// ---------------------------------------------------------------- transposed step
+// The Riccati step of the sweeps (k_lqr_backward_group, the fused MPC sweep)
+// with V_{t+1} held in registers, TRANSPOSED: lane l < n keeps column l of
+// V_{t+1} (= row l of V^T), lane n keeps v_{t+1}.  Then
+//   W  = V^T F   (lane l: its row times F; lane n: v^T F)     — one LDS exchange
+//   lane j reads column j of W and forms column j of F^T W = F^T V^T F, which
+//   is ROW j of P = F^T V F; its extra row n gives (F^T v)_j,
+// so lane j holds row j of Q = C + F^T V F and q_j = c_back_j + (F^T v)_j (the
+// reference's Q, q, lqr_step_explicit.py:96-101), and the new V_t column j /
+// v_t come from Q's columns (one more exchange).  Both products run over F's
+// nonzeros only when F's structure is known at compile time (the model's
+// Jacobian in registers, FS = Model::FSparsity: rocket 69 of 208 entries):
+// a zero term adds exactly nothing to an fma chain started at +0 (such a chain
+// never holds -0), so the dense F of the unfused path (FS = DenseF, rows in
+// LDS, DenseF of dilqr_device.h) gives the same bits on finite data.  Replaces per step the old rows-of-V
+// step's two dense 13x13x16 products and its V/F row broadcasts (group_riccati_step).
+template <int n, int m, bool HAS_F>
+struct GroupLdsT {
+  static constexpr int d = n + m;
+  static constexpr int W = 16;                   // padded row width (b128 reads)
+  float Wt[n + 1][W];                            // rows of V^T F, then v^T F
+  float Q[d][W + 4];                             // rows of Q, q at [.][W]
+  float Kk[m][W + 4];                            // gains K, k at [.][W] (box / pinverse modes)
+  float tau[W];
+  float tau2[W];
+  float F[HAS_F ? n : 1][W];                     // F rows (F from HBM)
+};
+
+// F as a lane sees it: registers (the model's Jacobian, every lane the whole
+// matrix) or the rows in LDS
+template <int n, int d>
+struct FRegs {
+  const float (&f)[n][d];
+  DEV float at(int k, int j) const { return f[k][j]; }
+};
+template <int n, int m>
+struct FRows {
+  const GroupLdsT<n, m, true>& L;
+  DEV float at(int k, int j) const { return L.F[k][j]; }
+};
+
+// One step.  U: this lane's column of V_{t+1} (lane n: v_{t+1}), replaced by
+// V_t's.  LAST (t = T-1): V_{t+1} = 0 and F = 0, so Q = C + 0, q = c_back + 0.
+// col: this lane's gain column (lane j < n: K[:, j], lanes >= n: k).
+template <int n, int m, int MODE, class FS, bool LAST, class FA, class LdsT>
+DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const float (&Crow)[n + m], float cb_r,
+                              const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&col)[m],
+                              float (&prev_k)[m], bool& have_prev, int& n_qp) {
+  constexpr int d = n + m, W = LdsT::W;
+  float Q[d], qr;
+  if constexpr (LAST) {
+#pragma unroll
+    for (int j = 0; j < d; ++j) Q[j] = Crow[j] + 0.f;
+    qr = cb_r + 0.f;
+  } else {
+    if (r <= n) {                                  // row r of V^T F (lane n: v^T F)
+      float Wr[d];
+#pragma unroll
+      for (int j = 0; j < d; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < n; ++k)
+          if (FS::nz(k, j)) s += U[k] * F.at(k, j);
+        Wr[j] = s;
+      }
+#pragma unroll
+      for (int j = 0; j < d; ++j) L.Wt[r][j] = Wr[j];
+    }
+    __syncthreads();
+    float Wc[n + 1];
+#pragma unroll
+    for (int l = 0; l <= n; ++l) Wc[l] = L.Wt[l][r];
+#pragma unroll
+    for (int i = 0; i < d; ++i) {                  // row r of F^T V F = column r of F^T (V^T F)
+      float s = 0.f;
+#pragma unroll
+      for (int l = 0; l < n; ++l)
+        if (FS::nz(l, i)) s += F.at(l, i) * Wc[l];
+      Q[i] = Crow[i] + s;
+    }
+    qr = cb_r + Wc[n];
+  }
+#pragma unroll
+  for (int j = 0; j < d; ++j) L.Q[r][j] = Q[j];
+  L.Q[r][W] = qr;
+  __syncthreads();
+  float Quu[m][m], qu[m], rhs[m];
+  const int jc = r <= n ? r : n;                   // this lane's right-hand side (lanes > n repeat k's)
+#pragma unroll
+  for (int a = 0; a < m; ++a) {
+#pragma unroll
+    for (int b = 0; b < m; ++b) Quu[a][b] = L.Q[n + a][n + b];
+    qu[a] = L.Q[n + a][W];
+    rhs[a] = jc < n ? L.Q[n + a][jc] : qu[a];
+  }
+  group_gains_col<n, m, MODE>(jc, Quu, rhs, qu, zI, lb, ub, col, prev_k, have_prev, n_qp);
+  // V_t column r (lane n: v_t), from column r of Q (lane n: q) and Q's u columns:
+  //   V[i][c] = ((Q[i][c] + sum_a Q[i][n+a] K[a][c]) + sum_a K[a][i] Q[n+a][c]) + sum_a K[a][i] (Quu K)[a][c]
+  // (lqr_step_explicit.py:157-160), v the same with q and k.  Unconstrained, K
+  // = -Quu^-1 Qux makes the last two terms cancel (K^T (Qux + Quu K) = 0): V =
+  // Qxx + Qxu K, v = q_x + Qxu k, and only this lane's own gain column is needed.
+  constexpr bool SCHUR = MODE == GAIN_UNC;
+  float Kall[m][n];
+  if constexpr (!SCHUR) {
+    if (r < n) {
+#pragma unroll
+      for (int a = 0; a < m; ++a) L.Kk[a][r] = col[a];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < m; ++a)
+#pragma unroll
+      for (int i = 0; i < n; ++i) Kall[a][i] = L.Kk[a][i];
+  }
+  if (r <= n) {
+    const int cx = r < n ? r : W;
+    float z[m], Qnc[m];
+    if constexpr (!SCHUR) {
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        float s = 0.f;
+#pragma unroll
+        for (int b = 0; b < m; ++b) s += Quu[a][b] * col[b];
+        z[a] = s;
+        Qnc[a] = L.Q[n + a][cx];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      float s1 = 0.f;
+#pragma unroll
+      for (int a = 0; a < m; ++a) s1 += L.Q[i][n + a] * col[a];
+      float vi = L.Q[i][cx] + s1;
+      if constexpr (!SCHUR) {
+        float s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int a = 0; a < m; ++a) {
+          s2 += Kall[a][i] * Qnc[a];
+          s3 += Kall[a][i] * z[a];
+        }
+        vi = (vi + s2) + s3;
+      }
+      U[i] = vi;
+    }
+  }
+}
+
 // standalone sweep, F from HBM (the LinDx / classic path and the north-star
-// kernel for rocket shapes)
+// kernel for rocket shapes): F's rows through LDS, dense
 template <int n, int m, int MODE>
 __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const float* __restrict__ C,
                                                            const float* __restrict__ c, const float* __restrict__ x,
@@ -250,24 +397,24 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
                                                            float* __restrict__ K, float* __restrict__ k,
                                                            int* __restrict__ n_qp) {
   constexpr int d = n + m;
-  __shared__ GroupLds<n, m> Ls[kGPW];
+  using LdsT = GroupLdsT<n, m, true>;
+  __shared__ LdsT Ls[kGPW];
   const int r = threadIdx.x & (kG - 1);
   const int gp = threadIdx.x / kG;
   const int b = blockIdx.x * kGPW + gp;
   const bool valid = b < B;
   const int bb = valid ? b : 0;
-  GroupLds<n, m>& L = Ls[gp];
-  if (r < n) {
+  LdsT& L = Ls[gp];
+  float U[n];
 #pragma unroll
-    for (int kk = 0; kk < GroupLds<n, m>::W; ++kk) L.V[r][kk] = 0.f;
-    L.v[r] = 0.f;
-  }
+  for (int i = 0; i < n; ++i) U[i] = 0.f;
   float prev_k[m];
 #pragma unroll
   for (int a = 0; a < m; ++a) prev_k[a] = 0.f;
   bool have_prev = false;
   int nqp = 0;
-  for (int t = T - 1; t >= 0; --t) {
+  auto step = [&](int t, auto last_c) {
+    constexpr bool LAST = decltype(last_c)::value;
     const size_t tb = (size_t)t * B + bb;
     float Crow[d], cb = 0.f, tau_r = 0.f;
 #pragma unroll
@@ -277,15 +424,12 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
       cb = c[tb * d + r];
       if (x) tau_r = r < n ? x[tb * n + r] : u[tb * m + (r - n)];
     }
-    if (r < n) {
-      if (t < T - 1) {
+    if constexpr (!LAST) {
+      if (r < n) {
         float Fr[d];
         ld(Fr, F + (tb * n + r) * d);
 #pragma unroll
         for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < d; ++j) L.F[r][j] = 0.f;
       }
     }
     if (r < d) L.tau[r] = tau_r;
@@ -307,17 +451,23 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
         ub[a] = bound_hi(bd, tb * m + a) - ut[a];
       }
     }
-    float Kt[m][n], kt[m];
-    group_riccati_step<n, m, MODE>(L, r, Crow, cb, zIt, lb, ub, Kt, kt, prev_k, have_prev, nqp);
+    float col[m];
+    group_riccati_step_t<n, m, MODE, DenseF, LAST>(L, r, FRows<n, m>{L}, U, Crow, cb, zIt, lb, ub, col, prev_k,
+                                                   have_prev, nqp);
     if (valid) {
       if (r < n) {
 #pragma unroll
-        for (int a = 0; a < m; ++a) K[tb * m * n + a * n + r] = L.Kk[a][r];
+        for (int a = 0; a < m; ++a) K[tb * m * n + a * n + r] = col[a];
       }
-      if (r < m) k[tb * m + r] = L.Kk[r][GroupLds<n, m>::W];
+      if (r == n) {
+#pragma unroll
+        for (int a = 0; a < m; ++a) k[tb * m + a] = col[a];
+      }
     }
     __syncthreads();
-  }
+  };
+  step(T - 1, std::true_type{});
+  for (int t = T - 2; t >= 0; --t) step(t, std::false_type{});
   if (valid && n_qp && r == 0) n_qp[b] = nqp;
 }
 
@@ -328,8 +478,8 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
 // shuffle-reduced from the per-row terms tau_r (C_r . tau) / 2 + c_r tau_r.
 // Dynamics: Model::forward_row (model rollout) or, with md == nullptr, the
 // LinDx step x' = F_t tau + f_t with F row r read by lane r.
-template <int n, int m, int GREC, class Model>
-DEV float group_forward_pass(GroupLds<n, m>& L, const Model* md, const float* __restrict__ F,
+template <int n, int m, int GREC, class Model, class LdsT>
+DEV float group_forward_pass(LdsT& L, const Model* md, const float* __restrict__ F,
                              const float* __restrict__ f, int T, int B, int b, int r, bool valid, float alpha,
                              const float* __restrict__ x_init, const float* __restrict__ C,
                              const float* __restrict__ c, const float* __restrict__ x, const float* __restrict__ u,
@@ -459,8 +609,8 @@ struct GroupCost {
 // Two step sizes rolled out together (the fused MPC kernel's paired line
 // search, see ilqr_problem): candidates A (alpha aA) and B (aB, if twoB) share
 // the step's loads; each keeps its own state component, controls and cost.
-template <int n, int m, int GREC, class Model>
-DEV void group_forward_pair(GroupLds<n, m>& L, const Model& md, int T, int B, int b, int r, bool valid, float aA,
+template <int n, int m, int GREC, class Model, class LdsT>
+DEV void group_forward_pair(LdsT& L, const Model& md, int T, int B, int b, int r, bool valid, float aA,
                             float aB, bool twoB, const float* __restrict__ x_init, const GroupCost& cs,
                             const float* __restrict__ x, const float* __restrict__ u,
                             const float* __restrict__ grec, const Bounds& bd, float* __restrict__ xa_out,
@@ -633,8 +783,8 @@ __global__ void __launch_bounds__(64) k_lqr_forward_group(int T, int B, const fl
 template <class Model>
 constexpr int group_grec() { return ((Model::M * Model::N + Model::M + 1) + 3) / 4 * 4; }
 
-template <class Model, int MODE>
-DEV void group_sweep(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r, bool valid, const Model& md,
+template <class Model, int MODE, class LdsT>
+DEV void group_sweep(LdsT& L, int T, int B, int b, int r, bool valid, const Model& md,
                      GroupCost& cs, const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd,
                      float* __restrict__ ws, float* __restrict__ cpk_out = nullptr,
                      unsigned char* __restrict__ sym_out = nullptr) {
@@ -642,19 +792,16 @@ DEV void group_sweep(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r
   bool ok_diag = true, ok_tinv = true;     // this lane's row: off-diagonal +0.0, equal to step T-1's
   float cd_last = 0.f, cc_last = 0.f;
   constexpr int GREC = group_grec<Model>();
-  constexpr int W = GroupLds<n, m>::W;
-  // ---------------- backward
-  if (r < n) {
+  float U[n];                              // column r of V_{t+1} (lane n: v_{t+1}), group_riccati_step_t
 #pragma unroll
-    for (int kk = 0; kk < W; ++kk) L.V[r][kk] = 0.f;
-    L.v[r] = 0.f;
-  }
+  for (int i = 0; i < n; ++i) U[i] = 0.f;
   float prev_k[m];
 #pragma unroll
   for (int a = 0; a < m; ++a) prev_k[a] = 0.f;
   bool have_prev = false;
   int nqp = 0;
-  for (int t = T - 1; t >= 0; --t) {
+  auto step = [&](int t, auto last_c) {
+    constexpr bool LAST = decltype(last_c)::value;
     const size_t tb = (size_t)t * B + b;
     float Crow[d], cr = 0.f, xt[n], ut[m];
     ld(xt, x + tb * n);                              // the group's 16 lanes read the same 64 B
@@ -667,21 +814,9 @@ DEV void group_sweep(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r
         if (j == r) dg = Crow[j];
         else ok_diag &= __float_as_uint(Crow[j]) == 0u;
       }
-      if (t == T - 1) { cd_last = dg; cc_last = cr; }
+      if (LAST) { cd_last = dg; cc_last = cr; }
       ok_tinv &= __float_as_uint(dg) == __float_as_uint(cd_last) && __float_as_uint(cr) == __float_as_uint(cc_last);
     }
-    if (r < n) {
-      float Fr[d];
-      if (t < T - 1) {
-        md.jac_row(r, xt, ut, Fr);
-      } else {
-#pragma unroll
-        for (int j = 0; j < d; ++j) Fr[j] = 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
-    }
-    __syncthreads();
     float tau[d];
 #pragma unroll
     for (int i = 0; i < n; ++i) tau[i] = xt[i];
@@ -704,19 +839,29 @@ DEV void group_sweep(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r
         ub[a] = bound_hi(bd, tb * m + a) - ut[a];
       }
     }
-    float Kt[m][n], kt[m];
-    group_riccati_step<n, m, MODE>(L, r, Crow, cb, zIt, lb, ub, Kt, kt, prev_k, have_prev, nqp);
+    float col[m];
+    // F_t = the model's Jacobian at (x_t, u_t), the whole matrix in every lane
+    // (uniform code; its structural zeros drop out of the products)
+    float Fu[n][d];
+    if constexpr (!LAST) md.jacobian(xt, ut, Fu);
+    group_riccati_step_t<n, m, MODE, typename Model::FSparsity, LAST>(L, r, FRegs<n, d>{Fu}, U, Crow, cb, zIt, lb, ub,
+                                                                     col, prev_k, have_prev, nqp);
     if (valid) {
       float* rec = ws + tb * GREC;
       if (r < n) {
 #pragma unroll
-        for (int a = 0; a < m; ++a) rec[a * n + r] = L.Kk[a][r];
+        for (int a = 0; a < m; ++a) rec[a * n + r] = col[a];
       }
-      if (r < m) rec[m * n + r] = L.Kk[r][W];
-      if (r == m) rec[m * n + m] = obj;
+      if (r == n) {
+#pragma unroll
+        for (int a = 0; a < m; ++a) rec[m * n + a] = col[a];
+      }
+      if (r == 0) rec[m * n + m] = obj;
     }
     __syncthreads();
-  }
+  };
+  step(T - 1, std::true_type{});
+  for (int t = T - 2; t >= 0; --t) step(t, std::false_type{});
   if (cpk_out) {
     // the group's verdict (all 16 rows), then the record and the flag; this
     // iteration's line search reads the registers already
@@ -735,8 +880,8 @@ DEV void group_sweep(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r
 // line-search rollout with row-distributed dynamics (Model::forward_row) and
 // shuffle-reduced costs.  (The rocket MPC iteration runs its line search one
 // problem per lane instead: dilqr_lane_search.h.)
-template <class Model, int MODE>
-DEV void group_ilqr_problem(GroupLds<Model::N, Model::M>& L, int T, int B, int b, int r, bool valid,
+template <class Model, int MODE, class LdsT>
+DEV void group_ilqr_problem(LdsT& L, int T, int B, int b, int r, bool valid,
                             const Model& md, const float* __restrict__ x_init, GroupCost cs,
                             const float* __restrict__ x, const float* __restrict__ u,
                             const Bounds& bd, float decay, int max_ls, float* __restrict__ ws,

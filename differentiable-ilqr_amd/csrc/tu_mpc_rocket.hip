@@ -15,7 +15,7 @@ __global__ void __launch_bounds__(64) k_ilqr_iterate_group(int T, int B, const f
                                                            float* __restrict__ cost_out, float* __restrict__ du_sq,
                                                            float* __restrict__ alpha_out,
                                                            const dilqr_mpc_ctrl* __restrict__ ctrl) {
-  __shared__ GroupLds<Model::N, Model::M> Ls[kGPW];
+  __shared__ GroupLdsT<Model::N, Model::M, false> Ls[kGPW];
   if (ctrl && ctrl->stopped) return;
   const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
   const int b0 = blockIdx.x * kGPW + gp;
@@ -45,7 +45,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_mpc_sweep_group(int 
                                                           Bounds bd, int iteration, float eps, int not_improved_lim,
                                                           int G, MpcState S) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
-  __shared__ GroupLds<n, m> Ls[kGPW];
+  __shared__ GroupLdsT<n, m, false> Ls[kGPW];
   if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   const bool first = iteration == 0;
   const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
