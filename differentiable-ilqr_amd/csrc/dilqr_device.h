@@ -212,8 +212,13 @@ DEV float eclamp(float x, float lo, float hi) {
 // sides, everything in registers (M<=4).  Used for Q_uu^{-1} (pinverse of a
 // nonsingular matrix), pnqp's masked LU (pnqp.py:53-54) and lu_solve of the
 // free block (lqr_step_explicit.py:150).
-template <int M, int R>
+// RCP: each pivot's reciprocal is v_rcp_f32 (1 ulp), formed once for the
+// elimination and the back substitution, instead of the IEEE division's
+// ~10-instruction sequence (the 16-lane group gain solves, one per lane per
+// step; results agree with the division to a few ulp).
+template <int M, int R, bool RCP = false>
 DEV void gauss_solve(float (&A)[M][M], float (&X)[M][R]) {
+  float invs[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) {
     // pivot search (compile-time indexed conditional swaps keep data in VGPRs)
@@ -233,7 +238,8 @@ DEV void gauss_solve(float (&A)[M][M], float (&X)[M][R]) {
         for (int j = 0; j < R; ++j) { float t = X[k][j]; X[k][j] = X[i][j]; X[i][j] = t; }
       }
     }
-    float inv = 1.0f / A[k][k];
+    float inv = RCP ? __builtin_amdgcn_rcpf(A[k][k]) : 1.0f / A[k][k];
+    invs[k] = inv;
 #pragma unroll
     for (int i = k + 1; i < M; ++i) {
       float l = A[i][k] * inv;
@@ -245,7 +251,7 @@ DEV void gauss_solve(float (&A)[M][M], float (&X)[M][R]) {
   }
 #pragma unroll
   for (int k = M - 1; k >= 0; --k) {
-    float inv = 1.0f / A[k][k];
+    const float inv = invs[k];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       float s = X[k][j];

@@ -81,7 +81,7 @@ DEV void group_gains_col(int j, const float (&Quu)[m][m], const float (&rhs)[m],
       X[a][0] = rhs[a];
     }
     if constexpr (MODE == GAIN_CHOL) chol_solve<m, 1>(A, X);
-    else gauss_solve<m, 1>(A, X);
+    else gauss_solve<m, 1, true>(A, X);
 #pragma unroll
     for (int a = 0; a < m; ++a) col[a] = -X[a][0];
   } else if constexpr (MODE == GAIN_ZERO_I) {
@@ -256,17 +256,33 @@ DEV void group_riccati_step(GroupLds<n, m>& L, int r, const float (&Crow)[n + m]
 // never holds -0), so the dense F of the unfused path (FS = DenseF, rows in
 // LDS, DenseF of dilqr_device.h) gives the same bits on finite data.  Replaces per step the old rows-of-V
 // step's two dense 13x13x16 products and its V/F row broadcasts (group_riccati_step).
-template <int n, int m, bool HAS_F>
+template <int n, int m, bool HAS_F, bool HAS_TAU>
 struct GroupLdsT {
   static constexpr int d = n + m;
-  static constexpr int W = 16;                   // padded row width (b128 reads)
+  static constexpr int W = 16;                   // padded row width (b128 accesses)
+  // Q row r: Q[r][0..d), q_r at [d].  Row stride: 16-byte aligned (W + 4) for
+  // the fused sweep (its u-column reads are one b128 per row), odd (d + 1) for
+  // the F-from-HBM sweep — measured at config 3 shapes, each layout is the
+  // faster one for its kernel (fused 0.407 vs 0.451 ms per MPC iteration,
+  // standalone 0.47 vs 0.56 ms)
+  static constexpr int QS = HAS_F ? d + 1 : W + 4;
   float Wt[n + 1][W];                            // rows of V^T F, then v^T F
-  float Q[d][W + 4];                             // rows of Q, q at [.][W]
-  float Kk[m][W + 4];                            // gains K, k at [.][W] (box / pinverse modes)
-  float tau[W];
-  float tau2[W];
+  float Q[d][QS];
+  float Kk[m][W];                                // gains K (box / pinverse modes: every lane needs all of K)
   float F[HAS_F ? n : 1][W];                     // F rows (F from HBM)
+  // The 4 groups of a wave use consecutive structs; a half-wave (32 lanes, the
+  // LDS's 32 banks) holds two of them, whose column reads (lane j: word j of a
+  // row) share banks unless the two bases differ by 16 words mod 32 (measured:
+  // the fused sweep 0.45 -> 0.41 ms per MPC iteration).  The padding is the
+  // tail of tau2, so a struct already at 16 mod 32 grows by nothing (the LDS
+  // per workgroup sets how many fit a CU).
+  static constexpr int kWords = (n + 1) * W + d * QS + m * W + (HAS_F ? n : 1) * W + 2 * (HAS_TAU ? W : 1);
+  static constexpr int kPad = ((16 - kWords % 32) % 32 + 32) % 32;
+  float tau[HAS_TAU ? W : 1];                    // tau / the line search's states
+  float tau2[(HAS_TAU ? W : 1) + kPad];
 };
+static_assert(sizeof(GroupLdsT<13, 3, false, false>) / 4 % 32 == 16, "bank offset between groups");
+static_assert(sizeof(GroupLdsT<13, 3, true, true>) / 4 % 32 == 16, "bank offset between groups");
 
 // F as a lane sees it: registers (the model's Jacobian, every lane the whole
 // matrix) or the rows in LDS
@@ -277,7 +293,7 @@ struct FRegs {
 };
 template <int n, int m>
 struct FRows {
-  const GroupLdsT<n, m, true>& L;
+  const GroupLdsT<n, m, true, true>& L;
   DEV float at(int k, int j) const { return L.F[k][j]; }
 };
 
@@ -288,7 +304,7 @@ template <int n, int m, int MODE, class FS, bool LAST, class FA, class LdsT>
 DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const float (&Crow)[n + m], float cb_r,
                               const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&col)[m],
                               float (&prev_k)[m], bool& have_prev, int& n_qp) {
-  constexpr int d = n + m, W = LdsT::W;
+  constexpr int d = n + m;
   float Q[d], qr;
   if constexpr (LAST) {
 #pragma unroll
@@ -324,7 +340,7 @@ DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const 
   }
 #pragma unroll
   for (int j = 0; j < d; ++j) L.Q[r][j] = Q[j];
-  L.Q[r][W] = qr;
+  L.Q[r][d] = qr;
   __syncthreads();
   float Quu[m][m], qu[m], rhs[m];
   const int jc = r <= n ? r : n;                   // this lane's right-hand side (lanes > n repeat k's)
@@ -332,7 +348,7 @@ DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const 
   for (int a = 0; a < m; ++a) {
 #pragma unroll
     for (int b = 0; b < m; ++b) Quu[a][b] = L.Q[n + a][n + b];
-    qu[a] = L.Q[n + a][W];
+    qu[a] = L.Q[n + a][d];
     rhs[a] = jc < n ? L.Q[n + a][jc] : qu[a];
   }
   group_gains_col<n, m, MODE>(jc, Quu, rhs, qu, zI, lb, ub, col, prev_k, have_prev, n_qp);
@@ -355,7 +371,7 @@ DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const 
       for (int i = 0; i < n; ++i) Kall[a][i] = L.Kk[a][i];
   }
   if (r <= n) {
-    const int cx = r < n ? r : W;
+    const int cx = r < n ? r : d;
     float z[m], Qnc[m];
     if constexpr (!SCHUR) {
 #pragma unroll
@@ -397,7 +413,7 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
                                                            float* __restrict__ K, float* __restrict__ k,
                                                            int* __restrict__ n_qp) {
   constexpr int d = n + m;
-  using LdsT = GroupLdsT<n, m, true>;
+  using LdsT = GroupLdsT<n, m, true, true>;
   __shared__ LdsT Ls[kGPW];
   const int r = threadIdx.x & (kG - 1);
   const int gp = threadIdx.x / kG;
@@ -825,10 +841,9 @@ DEV void group_sweep(LdsT& L, int T, int B, int b, int r, bool valid, const Mode
     float Ct = 0.f;
 #pragma unroll
     for (int j = 0; j < d; ++j) Ct += Crow[j] * tau[j];
-    float taur = 0.f;
-#pragma unroll
-    for (int j = 0; j < d; ++j) taur = (j == r) ? tau[j] : taur;
-    const float obj = group_sum(r < d ? 0.5f * (taur * Ct) + taur * cr : 0.f);
+    static_assert(d == kG, "lane r owns tau_r");
+    const float taur = r < n ? x[tb * n + r] : u[tb * m + (r - n)];   // tau[r], one load (no select chain)
+    const float obj = group_sum(0.5f * (taur * Ct) + taur * cr);
     const float cb = Ct + cr;
     float zIt[m], lb[m], ub[m];
 #pragma unroll

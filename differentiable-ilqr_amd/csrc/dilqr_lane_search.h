@@ -6,9 +6,9 @@
 // 13-vector: distributed over a group, its row-wise dynamics is a switch that
 // every lane of the wave executes case by case, the state goes through LDS at
 // every step, and the 4 problems of a wave pay 16 lanes of instructions each.
-// Here lane b rolls problem b's two candidates out (f2, Rocket::forward) from
-// the gain records the group sweep left in HBM, so a wave does 64 problems'
-// rollouts for the instructions the group kernel spent on 4.
+// Here a lane rolls one candidate of one problem out (Rocket::forward) from
+// the gain records the group sweep left in HBM, so a wave does 32 problems'
+// paired rollouts for the instructions the group kernel spent on 4.
 //
 // The arithmetic is the group line search's, bit for bit (group_forward_pair):
 // a 16-lane group_sum is a fixed butterfly, restated as tree16 below; each
@@ -48,24 +48,24 @@ struct LaneIn {
   }
 };
 
-// Stage cost of both candidates, tau = [x; u] (f2), the rows summed as
-// group_forward_pair does.  dconst: the time-invariant diagonal cost held in
+// Stage cost of this lane's candidate, tau = [x; u], the rows summed as
+// group_forward_pair does.  DCONST: the time-invariant diagonal cost held in
 // registers (cd, cc) — row r's product chain there is fma(C[r][j], tau_j, .)
 // over j with C[r][j] = +0 off the diagonal, which equals
 // fma(cd_r, tau_r, probe) with probe = that chain's +0 (NaN if any tau_j is
 // not finite: 0 * inf); otherwise the caller's C_t, c_t rows from HBM.
 template <int d, bool DCONST>
-DEV f2 lane_stage_cost(const f2 (&tau)[d], const float (&cd)[d], const float (&cc)[d],
-                       const float* __restrict__ C, const float* __restrict__ c, size_t tb) {
+DEV float lane_stage_cost(const float (&tau)[d], const float (&cd)[d], const float (&cc)[d],
+                          const float* __restrict__ C, const float* __restrict__ c, size_t tb) {
   static_assert(d == 16, "the group sum covers 16 rows");
-  f2 pr[d];
+  float pr[d];
   if constexpr (DCONST) {
-    f2 probe = f2{0.f, 0.f};
+    float probe = 0.f;
 #pragma unroll
-    for (int j = 0; j < d; ++j) probe = vfma(f2(0.f), tau[j], probe);
+    for (int j = 0; j < d; ++j) probe = __builtin_fmaf(0.f, tau[j], probe);
 #pragma unroll
     for (int r = 0; r < d; ++r) {
-      const f2 s = vfma(f2(cd[r]), tau[r], probe);
+      const float s = __builtin_fmaf(cd[r], tau[r], probe);
       pr[r] = 0.5f * (tau[r] * s) + tau[r] * cc[r];
     }
   } else {
@@ -73,7 +73,7 @@ DEV f2 lane_stage_cost(const f2 (&tau)[d], const float (&cd)[d], const float (&c
     for (int r = 0; r < d; ++r) {             // a dense cost: one row in registers at a time
       float Crow[d];
       ld(Crow, C + (tb * d + r) * d);
-      f2 s = f2{0.f, 0.f};
+      float s = 0.f;
 #pragma unroll
       for (int j = 0; j < d; ++j) s += Crow[j] * tau[j];
       pr[r] = 0.5f * (tau[r] * s) + tau[r] * c[tb * d + r];
@@ -82,124 +82,113 @@ DEV f2 lane_stage_cost(const f2 (&tau)[d], const float (&cd)[d], const float (&c
   return tree16(pr);
 }
 
-// One pass pair of the search (candidates A = alpha, B = alpha * decay, if
-// twoB), its stage costs summed into cA / cB and the current trajectory's
-// (from the gain records) into old_cost.  DCONST: the whole wave's problems
-// hold a time-invariant diagonal cost in registers (cd, cc), else every lane
-// reads the caller's rows (a flagged problem's rows hold the same values).
+// One pass of this lane's candidate (step size al; lane pair (A, B) of a
+// problem: passes 2p and 2p+1 of the search), its stage costs summed into
+// cost and the current trajectory's (from the gain records) into old_cost.
+// DCONST: the whole wave's problems hold a time-invariant diagonal cost in
+// registers (cd, cc), else every lane reads the caller's rows (a flagged
+// problem's rows hold the same values).  Writes x/u to (xo, uo) when `wr`.
 template <class Model, int BM, bool DCONST>
 DEV void lane_pass(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
                    const float (&cd)[Model::N + Model::M], const float (&cc)[Model::N + Model::M],
                    const float* __restrict__ C, const float* __restrict__ c, const float* __restrict__ ws,
-                   const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd, float aA, float aB,
-                   bool twoB, float* __restrict__ xa_out, float* __restrict__ ua_out, float* __restrict__ xb_out,
-                   float* __restrict__ ub_out, float* __restrict__ du_sq, float& cA, float& cB, float& old_cost) {
+                   const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd, float al, bool wr,
+                   float* __restrict__ xo, float* __restrict__ uo, float* __restrict__ du_sq, float& cost,
+                   float& old_cost) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
   constexpr int GREC = group_grec<Model>();
-  const f2 al = f2{aA, aB};
-  f2 xs[n];
-  {
-    float x0[n];
-    ld(x0, x_init + (size_t)b * n);
-    st(xa_out + (size_t)b * n, x0);
-    if (twoB) st(xb_out + (size_t)b * n, x0);
-#pragma unroll
-    for (int i = 0; i < n; ++i) xs[i] = f2{x0[i], x0[i]};
-  }
-  f2 sc = f2{0.f, 0.f};
-  float oldc = 0.f;
-  LaneIn<n, m, GREC> in, nx;
-  in.load(ws, x, u, 0, B, b);
-  for (int t = 0; t < T; ++t) {
+  float xs[n];
+  ld(xs, x_init + (size_t)b * n);
+  if (wr) st(xo + (size_t)b * n, xs);
+  float sc = 0.f, oldc = 0.f;
+  auto body = [&](int t, const LaneIn<n, m, GREC>& in) {
     const size_t tb = (size_t)t * B + b;
-    nx.load(ws, x, u, t + 1 < T ? t + 1 : t, B, b);                  // step t+1's inputs in flight
     oldc += in.g[m * n + m];
-    f2 nu[m];
+    float nu[m];
 #pragma unroll
     for (int a = 0; a < m; ++a) {
       // K dx with dx_t = x_t(new) - x_t(current), dx_0 = 0 (the group's dA
       // starts at 0: K * 0 keeps its sign); rows n.. of the group hold 0 * 0
-      f2 v[16];
+      float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const f2 dx = t > 0 ? xs[r < n ? r : 0] - in.x[r < n ? r : 0] : f2{0.f, 0.f};
-        v[r] = r < n ? in.g[a * n + r] * dx : f2{0.f, 0.f};
+        const float dx = t > 0 ? xs[r < n ? r : 0] - in.x[r < n ? r : 0] : 0.f;
+        v[r] = r < n ? in.g[a * n + r] * dx : 0.f;
       }
-      const f2 s = tree16(v);
+      const float s = tree16(v);
       nu[a] = (s + in.u[a]) + al * in.g[m * n + a];
-      if constexpr (BM != DILQR_BOUNDS_NONE) {
-        const float lo = bound_lo(bd, tb * m + a), hi = bound_hi(bd, tb * m + a);
-        nu[a] = f2{eclamp(nu[a].x, lo, hi), eclamp(nu[a].y, lo, hi)};
+      if constexpr (BM != DILQR_BOUNDS_NONE)
+        nu[a] = eclamp(nu[a], bound_lo(bd, tb * m + a), bound_hi(bd, tb * m + a));
+    }
+    if (wr) st(uo + tb * m, nu);
+    if (du_sq) {
+#pragma unroll
+      for (int a = 0; a < m; ++a) {
+        const float e = in.u[a] - nu[a];
+        du_sq[((size_t)t * m + a) * B + b] = e * e;
       }
     }
-    {
-      float ua[m], ub[m];
-#pragma unroll
-      for (int a = 0; a < m; ++a) { ua[a] = nu[a].x; ub[a] = nu[a].y; }
-      st(ua_out + tb * m, ua);
-      if (twoB) st(ub_out + tb * m, ub);
-      if (du_sq) {
-#pragma unroll
-        for (int a = 0; a < m; ++a) {
-          const float e = in.u[a] - ua[a];
-          du_sq[((size_t)t * m + a) * B + b] = e * e;
-        }
-      }
-    }
-    f2 tau[d];
+    float tau[d];
 #pragma unroll
     for (int i = 0; i < n; ++i) tau[i] = xs[i];
 #pragma unroll
     for (int a = 0; a < m; ++a) tau[n + a] = nu[a];
     sc += lane_stage_cost<d, DCONST>(tau, cd, cc, C, c, tb);
     if (t < T - 1) {
-      f2 xn[n];
+      float xn[n];
       md.forward(xs, nu, xn);
-      float xa[n], xb[n];
 #pragma unroll
-      for (int i = 0; i < n; ++i) {
-        xs[i] = xn[i];
-        xa[i] = xn[i].x;
-        xb[i] = xn[i].y;
-      }
-      st(xa_out + (tb + B) * n, xa);
-      if (twoB) st(xb_out + (tb + B) * n, xb);
+      for (int i = 0; i < n; ++i) xs[i] = xn[i];
+      if (wr) st(xo + (tb + B) * n, xs);
     }
-    in = nx;
+  };
+  // two input buffers in ping-pong (step t+1's loads in flight while step t
+  // computes; no copies between them)
+  LaneIn<n, m, GREC> b0, b1;
+  b0.load(ws, x, u, 0, B, b);
+  for (int t = 0; t < T; t += 2) {
+    if (t + 1 < T) b1.load(ws, x, u, t + 1, B, b);
+    body(t, b0);
+    if (t + 1 < T) {
+      if (t + 2 < T) b0.load(ws, x, u, t + 2, B, b);
+      body(t + 1, b1);
+    }
   }
-  cA = sc.x;
-  cB = sc.y;
+  cost = sc;
   old_cost = oldc;
 }
 
-// The MPC iteration's line search for problem b (lane b): paired passes 2p and
-// 2p+1 as in group_ilqr_problem, candidates into slots sa / sb, then the
-// best-iterate bookkeeping of k_mpc_iterate.  Runs after the group sweep
-// of the same iteration (k_mpc_sweep_group), which published the stop rule's
-// decision (ctrl[iteration & 1]) and, at iteration 0, the cost flags.
-template <class Model, int BM>
+// The MPC iteration's line search, one problem per LANE PAIR: lane 2b+0 rolls
+// candidate A (alpha) of problem b, lane 2b+1 candidate B (alpha * decay) —
+// passes 2p and 2p+1 of the search, as in group_ilqr_problem — into slots sa /
+// sb; the pair swaps costs and both take the same decision; then lane A does
+// the best-iterate bookkeeping of k_mpc_iterate.  (Both candidates as f2 in
+// one lane measured slower: 512 waves for 1024 SIMDs at config 3, 54 % of
+// wave time waiting on loads.)  Runs after the group sweep of the same
+// iteration (k_mpc_sweep_group), which published the stop rule's decision
+// (ctrl[iteration & 1]) and, at iteration 0, the cost flags.
+template <class Model, int BM, bool DCONST>
 __global__ void __launch_bounds__(64) k_mpc_search_lane(int T, int B, const float* __restrict__ theta,
                                                         const float* __restrict__ x_init,
                                                         const float* __restrict__ C, const float* __restrict__ c,
                                                         Bounds bd, float decay, int max_ls, int iteration,
                                                         float best_cost_eps, int G, MpcState S) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
-  constexpr int GREC = group_grec<Model>();
   if (iteration > 0 && G >= 0 && S.ctrl[iteration & 1].stopped) return;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = tid >> 1, cand = tid & 1;
+  if (b >= B) return;                                          // both lanes of a pair
   Model md; md.load(theta);
   const bool first = iteration == 0;
   const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
   const int cur = S.slot[b], best = S.slot[B + b];
   int sa, sb;
   free_slots(cur, best, sa, sb);
+  const int so = cand ? sb : sa;
   const float* x = S.Xs + cur * TBn;
   const float* u = S.Us + cur * TBm;
-  float* xa_out = S.Xs + sa * TBn;
-  float* ua_out = S.Us + sa * TBm;
-  float* xb_out = S.Xs + sb * TBn;
-  float* ub_out = S.Us + sb * TBm;
+  float* xo = S.Xs + so * TBn;
+  float* uo = S.Us + so * TBm;
   const bool dconst = S.Cpk && S.cost_sym[b] == 7;
   float cd[d], cc[d];
 #pragma unroll
@@ -208,26 +197,29 @@ __global__ void __launch_bounds__(64) k_mpc_search_lane(int T, int B, const floa
     ld(cd, S.Cpk + (size_t)b * 2 * d);
     ld(cc, S.Cpk + (size_t)b * 2 * d + d);
   }
-  // the register cost when every problem of the wave has one (wave-uniform)
-  const bool wave_dconst = __all(dconst);
+  // the register cost when every problem of the wave has one (wave-uniform);
+  // the two kinds of wave run in two instantiations (launched back to back,
+  // each leaves the other's waves at once), so that the dense-cost rollout's
+  // registers do not weigh on the common one
+  if (__all(dconst) != DCONST) return;
   float alpha = 1.f, cost = 0.f, old_cost = 0.f;
   int win = 0;
   for (int p = 0; p < max_ls; p += 2) {
     const bool twoB = p + 1 < max_ls;
     const float aA = alpha, aB = alpha * decay;
-    float cA, cB, oc;
-    float* dq = p == 0 ? S.du_sq : nullptr;
-    if (wave_dconst)
-      lane_pass<Model, BM, true>(T, B, b, md, x_init, cd, cc, C, c, S.ws, x, u, bd, aA, aB, twoB, xa_out, ua_out,
-                                 xb_out, ub_out, dq, cA, cB, oc);
-    else
-      lane_pass<Model, BM, false>(T, B, b, md, x_init, cd, cc, C, c, S.ws, x, u, bd, aA, aB, twoB, xa_out, ua_out,
-                                  xb_out, ub_out, dq, cA, cB, oc);
+    const float al = cand ? aB : aA;
+    const bool wr = !cand || twoB;                             // B rolls out only if pass p+1 exists
+    float cm, oc;
+    float* dq = (p == 0 && !cand) ? S.du_sq : nullptr;
+    lane_pass<Model, BM, DCONST>(T, B, b, md, x_init, cd, cc, C, c, S.ws, x, u, bd, al, wr, xo, uo, dq, cm, oc);
+    const float co = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(cm), 0xB1, 0xF, 0xF, false));
+    const float cA = cand ? co : cm, cB = cand ? cm : co;
     if (p == 0) old_cost = oc;
     if (!(cA > old_cost) || p == max_ls - 1) { cost = cA; alpha = aA; win = 0; break; }
     if (!(cB > old_cost) || p + 1 == max_ls - 1) { cost = cB; alpha = aB; win = 1; break; }
     alpha = aB * decay;                                       // lqr_step_explicit.py:249
   }
+  if (cand) return;
   const int nw = win ? sb : sa;
   S.cost[b] = cost;
   S.alpha[b] = alpha;

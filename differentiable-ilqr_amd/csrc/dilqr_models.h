@@ -225,34 +225,6 @@ struct Rocket {
 #pragma clang fp contract(off)
     return x[r] + deriv(r, x, u) * DT;
   }
-  // forward() of two trajectories at once (the line search's candidate pair,
-  // one problem per lane: dilqr_lane_search.h): every row of deriv() with the
-  // same expressions, so each f2 component rounds exactly like forward_row of
-  // its candidate; the shared scalars (1/mass, 1/J, l/2) are formed once
-  DEV void forward(const f2 (&x)[N], const f2 (&u)[M], f2 (&o)[N]) const {
-#pragma clang fp contract(off)
-    const f2 q0 = x[6], q1 = x[7], q2 = x[8], q3 = x[9], wx = x[10], wy = x[11], wz = x[12];
-    const float im = 1.f / mass;
-    const f2 Tx = vclamp(u[0], -400.f, 400.f), Ty = vclamp(u[1], -400.f, 400.f), Tz = vclamp(u[2], -400.f, 400.f);
-    f2 dd[N];
-    dd[0] = x[3]; dd[1] = x[4]; dd[2] = x[5];
-    dd[3] = (((1.f - 2.f * (q2 * q2 + q3 * q3)) * Tx + 2.f * (q1 * q2 - q0 * q3) * Ty) +
-             2.f * (q1 * q3 + q0 * q2) * Tz) * im + -10.f;
-    dd[4] = ((2.f * (q1 * q2 + q0 * q3) * Tx + (1.f - 2.f * (q1 * q1 + q3 * q3)) * Ty) +
-             2.f * (q2 * q3 - q0 * q1) * Tz) * im + 0.f;
-    dd[5] = ((2.f * (q1 * q3 - q0 * q2) * Tx + 2.f * (q2 * q3 + q0 * q1) * Ty) +
-             (1.f - 2.f * (q1 * q1 + q2 * q2)) * Tz) * im + 0.f;
-    dd[6] = 0.5f * (((-wx * q1) + (-wy * q2)) + (-wz * q3));
-    dd[7] = 0.5f * (((wx * q0) + (wz * q2)) + (-wy * q3));
-    dd[8] = 0.5f * (((wy * q0) + (-wz * q1)) + (wx * q3));
-    dd[9] = 0.5f * (((wz * q0) + (wy * q1)) + (-wx * q2));
-    dd[10] = (1.f / Jx) * (0.f - (wy * (Jz * wz) - wz * (Jy * wy)));
-    dd[11] = (1.f / Jy) * ((l / 2.f) * Tz - (wz * (Jx * wx) - wx * (Jz * wz)));
-    dd[12] = (1.f / Jz) * (-(l / 2.f) * Ty - (wx * (Jy * wy) - wy * (Jx * wx)));
-#pragma unroll
-    for (int r = 0; r < N; ++r) o[r] = x[r] + dd[r] * DT;
-  }
-
   // row r of get_linear_dyn (rocket.py:324-426), unclamped u.  RECIP: the
   // divisions by the mass and by J are products with reciprocals formed per
   // call (27 divisions over the 13 cases a 16-lane group executes -> 4); the

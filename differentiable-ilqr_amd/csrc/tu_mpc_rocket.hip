@@ -15,7 +15,7 @@ __global__ void __launch_bounds__(64) k_ilqr_iterate_group(int T, int B, const f
                                                            float* __restrict__ cost_out, float* __restrict__ du_sq,
                                                            float* __restrict__ alpha_out,
                                                            const dilqr_mpc_ctrl* __restrict__ ctrl) {
-  __shared__ GroupLdsT<Model::N, Model::M, false> Ls[kGPW];
+  __shared__ GroupLdsT<Model::N, Model::M, false, true> Ls[kGPW];
   if (ctrl && ctrl->stopped) return;
   const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
   const int b0 = blockIdx.x * kGPW + gp;
@@ -40,12 +40,15 @@ __global__ void __launch_bounds__(64) k_ilqr_iterate_group(int T, int B, const f
 // doing both took 1.08 ms per iteration, its row-distributed rollout being the
 // larger half.
 template <class Model, int MODE>
-__global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_mpc_sweep_group(int T, int B, const float* __restrict__ theta,
+#ifndef DILQR_SWEEP_WAVES
+#define DILQR_SWEEP_WAVES 3
+#endif
+__global__ void __launch_bounds__(64, DILQR_SWEEP_WAVES) k_mpc_sweep_group(int T, int B, const float* __restrict__ theta,
                                                           const float* __restrict__ C, const float* __restrict__ c,
                                                           Bounds bd, int iteration, float eps, int not_improved_lim,
                                                           int G, MpcState S) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
-  __shared__ GroupLdsT<n, m, false> Ls[kGPW];
+  __shared__ GroupLdsT<n, m, false, false> Ls[kGPW];
   if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   const bool first = iteration == 0;
   const int r = threadIdx.x & (kG - 1), gp = threadIdx.x / kG;
@@ -68,17 +71,21 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_mpc_sweep_group(int 
 }
 
 int launch_mpc_step_rocket(const MpcStepArgs& a) {
+#define SEARCH(BM_, DC_)                                                                                          \
+  k_mpc_search_lane<Rocket, BM_, DC_><<<grid_for(2 * (long long)a.B), kBlock, 0, a.stream>>>(                     \
+      a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st)
   if (a.bd.mode != DILQR_BOUNDS_NONE) {
     k_mpc_sweep_group<Rocket, GAIN_BOX><<<grid_group(a.B), 64, 0, a.stream>>>(
         a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st);
-    k_mpc_search_lane<Rocket, DILQR_BOUNDS_SCALAR><<<grid_for(a.B), kBlock, 0, a.stream>>>(
-        a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st);
+    SEARCH(DILQR_BOUNDS_SCALAR, true);
+    SEARCH(DILQR_BOUNDS_SCALAR, false);
   } else {
     k_mpc_sweep_group<Rocket, GAIN_UNC><<<grid_group(a.B), 64, 0, a.stream>>>(
         a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st);
-    k_mpc_search_lane<Rocket, DILQR_BOUNDS_NONE><<<grid_for(a.B), kBlock, 0, a.stream>>>(
-        a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st);
+    SEARCH(DILQR_BOUNDS_NONE, true);
+    SEARCH(DILQR_BOUNDS_NONE, false);
   }
+#undef SEARCH
   return launched();
 }
 
