@@ -59,7 +59,11 @@ struct GroupLds {
   float Qu[m][W + 4];                          // u rows of Q, q_u at [.][W]
   float Kk[m][W + 4];                          // gains K, k at [.][W]
   float tau[W];
-  float tau2[W];                               // the paired line search's second candidate
+  // tau2: the paired line search's second candidate; its tail pads the struct
+  // to 16 words mod 32, so the two groups of a half-wave read columns from
+  // disjoint LDS banks (see GroupLdsT)
+  static constexpr int kWords = 2 * n * W + W + 2 * m * (W + 4) + 2 * W;
+  float tau2[W + ((16 - kWords % 32) % 32 + 32) % 32];
 };
 
 // Gains from the u-rows of Q (modes as RiccatiState::step), distributed over

@@ -35,7 +35,11 @@ template <int n, int p>
 struct ImplicitGroupLds {
   float gx[n][p + 1];                          // gradx_{t-1} (phase A)
   float vec[kG];                               // lam_{t+1} (B) / y_t (C, D)
-  float dlam[kG];                              // dlam_{t+1} (D)
+  // dlam_{t+1} (D); the tail makes the struct an odd number of words mod 32,
+  // so the gx rows of a half-wave's two groups (stride p+1 words) fall on
+  // disjoint banks
+  static constexpr int kWords = n * (p + 1) + 2 * kG;
+  float dlam[kG + ((kWords % 2) ? 0 : 1)];
 };
 
 template <class Model, class D2, int MODE>
