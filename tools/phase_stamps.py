@@ -8,6 +8,7 @@ old cost), line search, epilogue.  The clock is s_memtime / s_memrealtime
 
   make -C differentiable-ilqr_amd stamps      # here, on the CPU
   python tools/phase_stamps.py [iteration]     # on the GPU box
+  BOUNDS=100 python tools/phase_stamps.py       # config 4 (box +-100)
 """
 import ctypes
 import json
@@ -35,7 +36,8 @@ C = torch.diag(torch.tensor(q)).repeat(T, B, 1, 1).to(dev).contiguous()
 c = torch.tensor(p).repeat(T, B, 1).to(dev).contiguous()
 theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
 sv = ops.MPCSolve(T, B, n, m, dev)
-nb, _keep = N.make_bounds(None, None)
+LIM = float(os.environ.get("BOUNDS", "0"))
+nb, _keep = N.make_bounds(-LIM, LIM) if LIM > 0 else N.make_bounds(None, None)
 s = N.stream(dev)
 W = B // 64
 lib = N.lib()
@@ -56,18 +58,20 @@ for solve in range(4):
         N.call("dilqr_mpc_stop_rule_f32", T, m, B, i, sv.state, s)
     torch.cuda.synchronize()
 
-out = {"iteration": STOP_AT, "waves": W}
+out = {"iteration": STOP_AT, "waves": W, "bounds": LIM or None}
 r = rows[-1]
 ghz = (r[:, 4] - r[:, 0]) / ((r[:, 7] - r[:, 6]) / 100e6) / 1e9
 out["clock_ghz_median"] = float(np.median(ghz))
 for name, a, b_ in (("prologue", 0, 1), ("sweep", 1, 2), ("line_search", 2, 3), ("epilogue", 3, 4), ("wave", 0, 4)):
     cyc = np.concatenate([x[:, b_] - x[:, a] for x in rows[1:]])
     out[name + "_cycles"] = {"median": float(np.median(cyc)), "p10": float(np.percentile(cyc, 10)),
-                             "p90": float(np.percentile(cyc, 90))}
+                             "p90": float(np.percentile(cyc, 90)), "max": float(cyc.max())}
     out[name + "_us_median"] = float(np.median(cyc) / (out["clock_ghz_median"] * 1e3))
 span = [(x[:, 7].max() - x[:, 6].min()) / 100.0 for x in rows[1:]]           # us, 100 MHz ticks
 start_spread = [(x[:, 6].max() - x[:, 6].min()) / 100.0 for x in rows[1:]]
 out["kernel_span_us"] = float(np.median(span))
+end_spread = [(x[:, 7].max() - x[:, 7].min()) / 100.0 for x in rows[1:]]
+out["wave_end_spread_us"] = float(np.median(end_spread))
 out["wave_start_spread_us"] = float(np.median(start_spread))
 out["per_step_cycles"] = {"sweep": out["sweep_cycles"]["median"] / T, "line_search": out["line_search_cycles"]["median"] / T}
 print(json.dumps(out))
