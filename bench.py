@@ -340,11 +340,13 @@ def secondary_configs(dev):
     out["config3_rocket"] = {
         "value": val, "unit": "problem-iters/s", "ms_per_iter": ms_it, "batch": B, "T": T,
         "fused_iteration": with_pmc(
-            {"kernel": "k_mpc_sweep_group<Rocket,UNC> + k_mpc_search_lane<Rocket,NONE> (one MPC iteration of "
-                       "the timed solves, steady state)",
+            {"kernel": "k_mpc_sweep_group<Rocket,UNC> + k_mpc_search_lane<Rocket,NONE,register cost> (+ the "
+                       "dense-cost instantiation, which leaves at once): one MPC iteration of the timed solves, "
+                       "steady state",
              "bound": "hbm", "avg_launch_ms": it_ms, "algorithmic_bytes_per_launch": it_bytes,
              "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
-            ("k_mpc_sweep_group<Rocket, 0>", "k_mpc_search_lane<Rocket, 0>")),
+            ("k_mpc_sweep_group<Rocket, 0>", "k_mpc_search_lane<Rocket, 0, true>",
+             "k_mpc_search_lane<Rocket, 0, false>")),
         "riccati_sweep": sweep_roofline(n, m, T, B, dev)}
     # rocket implicit backward (16-lane groups) at the solution of the timed solves
     x, u = sv.gather_best()
