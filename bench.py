@@ -4,18 +4,20 @@
 BASELINE.json metric: "iLQR iters/sec (whole node), batch=65536 cartpole T=25 at
 1/2/4/8 MI355X" (configs[1]; configs[4] = the same at 8 GPUs, sharded).
 
-A step = one iLQR iteration of mpc_explicit.MPC.forward (mpc_explicit.py:246-299)
-over the rank's 65536 problems: rollout-linearise-Riccati-line search (one fused
-kernel) + best-iterate/stop bookkeeping.  Steps run as whole solves from u = 0
-(lqr_iter = 10 per solve, the MPC default; the initial rollout of each solve is
-inside the timed region).  eps = 0 and not_improved_lim = inf keep every
-iteration live (the reference's own fixed-iteration protocol).
+A step = one whole mpc_explicit.MPC.forward solve (mpc_explicit.py:228-299) over
+the rank's 65536 problems from u = 0: the initial rollout and lqr_iter = 10
+iLQR iterations (rollout-linearise-Riccati-line search + best-iterate
+bookkeeping each), the MPC default.  eps = 0 and not_improved_lim = inf keep
+every iteration live (the reference's own fixed-iteration protocol,
+BASELINE.md), so each solve is ONE dilqr_mpc_solve_fixed_f32 call: begin and
+all ten iterations in one launch (each lane iterates its own problem), plus
+the best_du finish launch.  value = problems x iterations / s.
 
 Multi-GPU: one process per GPU (torchrun); problems shard as contiguous slices
 of the one generated set; no collective in the data path (weak scaling).  The
 barrier + synchronize bracket the timed region; the time is the MAX over ranks.
 
-Prints ONE JSON line on rank 0 with `roofline` (fused iteration kernel, HIP
+Prints ONE JSON line on rank 0 with `roofline` (the whole-solve launch, HIP
 events on its stream) and `cpu_baseline` (the reference's CPU PyTorch op
 structure restated in fp32 torch, oracle/torch_cpu.py, on the host cores).
 """
@@ -62,6 +64,24 @@ def iter_cost_floats(flags, T=T_HORIZON, d=D):
 
 def iter_bytes_per_problem(cost_floats, T=T_HORIZON, n=N_STATE, d=D):
     return 4 * (cost_floats + n + 2 * T * d + 2)
+
+
+def solve_bytes_per_problem(flags, iters, T=T_HORIZON, n=N_STATE, m=N_CTRL, d=D):
+    """Algorithmic bytes of one fixed-count solve (dilqr_mpc_solve_fixed_f32), per
+    problem: begin (x_init in, slot 0 out), iteration 0 (the caller's C, c in, the
+    packed copy out: one record for a time-invariant cost), iterations 1..iters-1
+    (the cost as iter_cost_floats reads it), each iteration x_init, the current
+    trajectory in, the new one out, its du rows, cost and du_norm; the finish
+    (two du rows in, best_du and full_du_norm out)."""
+    pk = d * (d + 1) // 2 + d
+    f = np.asarray(flags).astype(np.int64)
+    packed_out = np.where((f & 4) != 0, pk, T * pk)
+    per_iter = n + 2 * T * d + T * m + 2
+    floats = ((n + T * d)
+              + (T * (d * d + d) + packed_out + per_iter)
+              + (iters - 1) * (iter_cost_floats(f, T, d) + per_iter)
+              + (2 * T * m + 2))
+    return 4 * floats
 #  Riccati sweep, per problem: C, c_back, F in; K, k out
 SWEEP_BYTES_PER_PROBLEM = 4 * (T_HORIZON * D * D + T_HORIZON * D + (T_HORIZON - 1) * N_STATE * D
                                + T_HORIZON * N_CTRL * N_STATE + T_HORIZON * N_CTRL)                  # 7,680
@@ -104,12 +124,10 @@ def _timed_solves(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, lqr_iter
     from dilqr import _native as N
 
     def solve():
-        sv.begin(model_id, theta, x0)
         if sv.fixed_iters == lqr_iter:                  # the stop rule cannot fire: fixed-count solve
-            for i in range(lqr_iter):
-                sv.iterate_fixed(model_id, theta, x0, C, c, bounds, decay, max_ls, i, 1e-4)
-            sv.finish_fixed(lqr_iter)
+            sv.solve_fixed(model_id, theta, x0, C, c, bounds, decay, max_ls, 1e-4)
             return
+        sv.begin(model_id, theta, x0)
         for i in range(lqr_iter):
             sv.iterate(model_id, theta, x0, C, c, bounds, decay, max_ls, i, 1e-4, 0.0, 10 ** 9)
     for _ in range(warmup_solves):
@@ -131,6 +149,10 @@ def _event_ms(stream, fn, reps):
     several us of its own to a 40-us kernel; rocprof's kernel durations agree
     with this figure, profiles/)."""
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # the stream sleeps (~5 ms) while the host queues every launch, so the event
+    # pair times the kernels back to back, not the host's launch rate (a ctypes
+    # launch takes tens of us of Python, comparable to one 36-us iteration)
+    torch.cuda._sleep(10_000_000)
     e0.record(stream)
     for r in range(reps):
         fn(r)
@@ -537,29 +559,20 @@ def main():
     c = torch.tensor(p).repeat(T_HORIZON, B, 1).to(dev).contiguous()
     theta = torch.tensor([9.8, 1.0, 0.1, 0.5], device=dev)
     # eps = 0 and not_improved_lim = 1e9: the stop rule cannot fire, so the
-    # solve is a fixed-count one (ops.mpc_solve takes the same path): one launch
-    # per iteration, best_du formed by finish_fixed at the end of each solve
+    # solve is a fixed-count one (ops.mpc_solve takes the same path): begin and
+    # every iteration in one launch, best_du formed by the finish launch
     sv = ops.MPCSolve(T_HORIZON, B, N_STATE, N_CTRL, dev, fixed_iters=args.lqr_iter)
     bounds, _ = N.make_bounds(None, None)
     stream = torch.cuda.current_stream(dev)
     s = N.stream(dev)
 
-    state = {"i": 0}
-
-    def step():
-        it = state["i"] % args.lqr_iter
-        if it == 0:
-            sv.begin(N.MODEL_CARTPOLE, theta, x0)
-        sv.iterate_fixed(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, it, 1e-4)
-        if it == args.lqr_iter - 1:
-            sv.finish_fixed(args.lqr_iter)
-        state["i"] += 1
+    def step():                 # one MPC.forward solve of lqr_iter iterations
+        sv.solve_fixed(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, 1e-4)
 
     if args.kernels_only:
         args.steps, args.warmup, args.no_cpu_baseline, args.no_secondary = 0, 2, True, True
     for _ in range(args.warmup):
         step()
-    state["i"] = 0
     torch.cuda.synchronize(dev)
     if dist:
         tdist.barrier()
@@ -583,12 +596,17 @@ def main():
         torch.save({"rows": (lo, hi), "x": xb.cpu(), "u": ub.cpu(), "cost": sv.best_cost.cpu()},
                    os.path.join(args.dump, f"shard{rank}.pt"))
 
-    # ---- roofline of the dominant kernel: the steady-state fused MPC iteration
-    # kernel (k_mpc_iterate<..., FIRST=false>), iterations 1..reps of a solve
-    # launched back to back between one pair of HIP events on ITS stream (the
-    # current stream, where ops launch it).  No stop-rule launches in between:
-    # with eps = 0 and not_improved_lim = inf the rule cannot fire.
+    # ---- roofline of the dominant kernel: the whole-solve launch
+    # (k_mpc_solve_fixed + its finish, one dilqr_mpc_solve_fixed_f32 call = one
+    # step), reps solves back to back between one pair of HIP events on ITS
+    # stream (the current stream, where ops launch it)
     reps = 10
+    solve_ms = _event_ms(stream, lambda r: step(), reps)
+    solve_bytes = float(solve_bytes_per_problem(sv.cost_sym.cpu().numpy(), args.lqr_iter).sum())
+    # ---- the per-iteration kernel of the stop-rule path (k_mpc_iterate<...,
+    # FIRST=false>): iterations 1..reps of a solve launched back to back.  No
+    # stop-rule launches in between: with eps = 0 and not_improved_lim = inf the
+    # rule cannot fire.
     sv.begin(N.MODEL_CARTPOLE, theta, x0)
     sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
     iter_ms = _event_ms(stream, lambda r: N.call(
@@ -618,16 +636,22 @@ def main():
     # bytes per launch with the gfx950 FETCH_SIZE correction, and the issue
     # breakdown (what bounds the kernel: VALU issue, not HBM)
     pmc = load_pmc()
-    head_pmc = pmc.get("k_mpc_iterate<Cartpole, 0, true, false>", {})
-    traffic = head_pmc.get("hbm_bytes_per_launch")
-    traffic = None if traffic is None else traffic * B / B_PER_GPU
+    head_pmc = pmc.get("k_mpc_solve_fixed<Cartpole, 0, true>", {})
+    fin_pmc = pmc.get("k_mpc_fixed_finish", {})
+    traffic = None
+    if "hbm_bytes_per_launch" in head_pmc and "hbm_bytes_per_launch" in fin_pmc:
+        traffic = (head_pmc["hbm_bytes_per_launch"] + fin_pmc["hbm_bytes_per_launch"]) * B / B_PER_GPU
+    it_pmc = pmc.get("k_mpc_iterate<Cartpole, 0, true, false>", {})
+    it_traffic = it_pmc.get("hbm_bytes_per_launch")
+    it_traffic = None if it_traffic is None else it_traffic * B / B_PER_GPU
     dense = None if args.kernels_only or world > 1 else dense_cost_roofline(dev, x0, theta, B)
 
     if rank == 0 and args.kernels_only:
-        print(json.dumps({"iter_ms": iter_ms, "sweep_ms": sweep_ms}), flush=True)
+        print(json.dumps({"solve_ms": solve_ms, "iter_ms": iter_ms, "sweep_ms": sweep_ms}), flush=True)
     elif rank == 0:
-        value = B_total * args.steps / elapsed
-        achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
+        value = B_total * args.lqr_iter * args.steps / elapsed
+        achieved = solve_bytes / (solve_ms * 1e-3) / 1e9
+        it_achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
         sweep_gbs = sweep_bytes / (sweep_ms * 1e-3) / 1e9
         line = {
             "metric": "iLQR iters/sec (whole node), batch=65536 cartpole T=25 at 1/2/4/8 MI355X",
@@ -637,6 +661,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
+            "ms_per_iteration": elapsed * 1e3 / (args.steps * args.lqr_iter),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -644,18 +669,26 @@ def main():
             "data": "synthetic (SURVEY.md §8(d) config 2 x_init, seed 0; cartpole get_true_obj cost materialised "
                     "per (t,b))",
             "config": {"workload": "cartpole n=5 m=1 T=25, unconstrained iLQR, 65536 problems per GPU, "
-                                   f"whole-batch solves of lqr_iter={args.lqr_iter} from u=0",
-                       "batch_per_gpu": B, "global_batch": B_total, "T": T_HORIZON,
+                                   f"step = one whole-batch MPC solve of lqr_iter={args.lqr_iter} from u=0",
+                       "batch_per_gpu": B, "global_batch": B_total, "T": T_HORIZON, "lqr_iter": args.lqr_iter,
                        "parallelism": f"batch-sharded x{world} (no collective)",
-                       "batch_iters_per_s": world * args.steps / elapsed},
-            "roofline": {"kernel": "k_mpc_iterate<Cartpole,UNC,LDS gains,steady> (fused linearise+Riccati+line search; "
-                                   + cost_path + ")",
+                       "batch_iters_per_s": world * args.lqr_iter * args.steps / elapsed},
+            "roofline": {"kernel": "k_mpc_solve_fixed<Cartpole,UNC,LDS gains> + k_mpc_fixed_finish (one whole "
+                                   "fixed-count solve: begin + iteration 0 reading the caller's C + "
+                                   f"{args.lqr_iter - 1} steady iterations; " + cost_path + ")",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_measured_at": PMC_COMMIT[0],
-                         "algorithmic_bytes_per_launch": iter_bytes, "avg_launch_ms": iter_ms,
+                         "algorithmic_bytes_per_launch": solve_bytes, "avg_launch_ms": solve_ms,
                          "limiter": {"what": "VALU issue at one wave per SIMD (B=65536 = 1024 waves); not HBM",
                                      **{k: v for k, v in head_pmc.items() if k != "hbm_bytes_per_launch"}}},
+            "roofline_steady_iteration": {
+                "kernel": "k_mpc_iterate<Cartpole,UNC,LDS gains,steady> (the stop-rule path's per-iteration launch; "
+                          + cost_path + ")",
+                "bound": "hbm", "achieved": it_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": it_achieved / HBM_PEAK_GBS, "traffic": it_traffic, "algorithmic_bytes_per_launch": iter_bytes,
+                "avg_launch_ms": iter_ms,
+                "pmc": {k: v for k, v in it_pmc.items() if k != "hbm_bytes_per_launch"}},
             "roofline_dense_cost": dense,
             "riccati_roofline": {"kernel": "k_lqr_backward<5,1,UNC> (standalone sweep, F from HBM)",
                                  "bound": "hbm", "achieved": sweep_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -475,7 +475,7 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
 // records a later change of the cost proves necessary are written then, from
 // the registers holding that record), and a time-invariant diagonal cost is
 // handed to this iteration's line search in registers, so C is read once.
-// PREV: the current trajectory's cost is prev_cost[b], the cost the previous
+// PREV: the current trajectory's cost is prev_cost, the cost the previous
 // MPC iteration's line search computed for it (the accepted candidate), so the
 // sweep forms only C tau for c_back and not the stage costs again.
 template <class Model, int BM, int TL, bool ROLLOUT, class CostT, bool PREV = false>
@@ -485,13 +485,13 @@ DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restric
                      const GainRecs& ws, float* __restrict__ xa_out, float* __restrict__ ua_out,
                      float* __restrict__ xb_out, float* __restrict__ ub_out, float* __restrict__ du_sq,
                      float& cost_out, float& alpha_out, bool b_in_gains = false,
-                     const float* __restrict__ prev_cost = nullptr) {
+                     float prev_cost = 0.f, unsigned* flags_out = nullptr) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
   constexpr int MODE = BM == DILQR_BOUNDS_NONE ? GAIN_UNC : GAIN_BOX;
   constexpr int GREC = m * n + m;                    // gain record: K, k (component-major)
   constexpr int PK = packed_cost_floats<d>();
   float old_cost = 0.f;                               // the current trajectory's cost, from the sweep
-  if constexpr (PREV) old_cost = prev_cost[b];        // ... or from the previous line search
+  if constexpr (PREV) old_cost = prev_cost;           // ... or from the previous line search
   bool sym = true, diag = true, tinv = true;
   bool symsofar = true;                               // C_t' bitwise symmetric for all t' >= t (RiccatiState SYM)
   float pk_last[PK];                                  // step T-1's packed record (tinv test)
@@ -592,10 +592,13 @@ DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restric
     sweep_step(T - 1, std::true_type{});
 #pragma unroll 2
     for (int t = T - 2; t >= 0; --t) sweep_step(t, std::false_type{});
-    if (sym_out)
-      sym_out[b] = sym ? (unsigned char)(kCostSym | (diag && packed_diag_ok<d>() ? kCostDiag : 0) |
-                                         (tinv ? kCostTinv : 0))
-                       : 0;
+    if (sym_out) {
+      const unsigned char f = sym ? (unsigned char)(kCostSym | (diag && packed_diag_ok<d>() ? kCostDiag : 0) |
+                                                    (tinv ? kCostTinv : 0))
+                                  : 0;
+      sym_out[b] = f;
+      if (flags_out) *flags_out = f;                    // (a local of an inlined caller: a register)
+    }
   }
   DILQR_STAMP(2);
   if constexpr (!CostT::kDiag && packed_diag_ok<d>()) {
@@ -669,32 +672,28 @@ DEV void free_slots(int cur, int best, int& sa, int& sb) {
   }
 }
 
+// One MPC iteration of problem b (this lane) on its trajectory slots: the
+// fused linearise + sweep + line search into the two free slots.  The caller
+// holds the problem's state — cur/best slot, its cost flags pk (steady
+// iterations), the current trajectory's cost prev_cost (the previous line
+// search's) — and does the best-iterate bookkeeping with the result.
 // LG: the gain records live in this workgroup's LDS (dynamic, T*64*GREC floats;
-// dilqr_mpc_step_f32 picks it when 4 workgroups per CU still fit the 160 KB),
-// instead of a workspace round trip through HBM/MALL every iteration.
+// picked when 4 workgroups per CU still fit the 160 KB), instead of a workspace
+// round trip through HBM/MALL every iteration.
 // FIRST: iteration 0 of the solve (reads the caller's C, c and builds the
-// packed copy) — its own instantiation, so the steady-state kernel carries no
-// copy-building code and profiles separately.
+// packed copy; its cost flags come back in *flags_out).
+struct LaneIter {
+  float cost, alpha;
+  int slot;                                                 // the accepted candidate's slot
+};
+
 template <class Model, int BM, bool LG, bool FIRST>
-__global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const float* __restrict__ theta,
-                                                        const float* __restrict__ x_init, const float* __restrict__ C,
-                                                        const float* __restrict__ c, Bounds bd, float decay, int max_ls,
-                                                        int iteration, float best_cost_eps, float eps,
-                                                        int not_improved_lim, int G, MpcState S) {
+DEV LaneIter mpc_iteration_lane(int T, int B, int b, const Model md, const float* __restrict__ x_init,
+                                const float* __restrict__ C, const float* __restrict__ c, const Bounds& bd,
+                                float decay, int max_ls, const MpcState& S, float* __restrict__ du_sq,
+                                float* __restrict__ lds_gains, int cur, int best, unsigned pk, float prev_cost,
+                                unsigned* flags_out = nullptr) {
   constexpr int n = Model::N, m = Model::M;
-  constexpr bool first = FIRST;                             // == (iteration == 0), chosen by the host
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  // the problem's slot indices and cost flags are read together with the stop
-  // rule's inputs (one memory latency in the prologue, not three)
-  const int bl = b < B ? b : B - 1;
-  const int cur = S.slot[bl], best = S.slot[B + bl];
-  const unsigned char pk = (!FIRST && S.Cpk) ? S.cost_sym[bl] : 0;
-  DILQR_STAMP(0);
-  DILQR_STAMP(6);
-  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
-  if (b >= B) return;
-  DILQR_STAMP(1);
-  Model md; md.load(theta);
   const size_t TBd = (size_t)T * B * (n + m);               // one slot: [T,B,d] records
   int sa, sb;
   free_slots(cur, best, sa, sb);
@@ -703,7 +702,6 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   float* xsb = S.Xs + sb * TBd;
   float cost, alpha;
   int win;
-  extern __shared__ __attribute__((aligned(16))) float lds_gains[];
   const GainRecs gr = LG ? GainRecs{lds_gains, kBlock, (int)threadIdx.x} : GainRecs{S.ws, B, b};
   // the solve's packed symmetric cost: built by iteration 0's sweep (which reads
   // C, c), used from iteration 1 on by every problem whose C_t are all bitwise
@@ -716,15 +714,15 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
   if constexpr (FIRST) {
     win = ilqr_problem<Model, BM, TRAJ_REC, true>(T, B, b, md, x_init, full, S.Cpk, S.Cpk ? S.cost_sym : nullptr,
                                                   xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
-                                                  S.du_sq, cost, alpha, b_lds);
+                                                  du_sq, cost, alpha, b_lds, 0.f, flags_out);
   } else {
     if ((pk & (kCostDiag | kCostTinv)) == (kCostDiag | kCostTinv)) {
       if constexpr (packed_diag_ok<n + m>()) {
         CostDiagConst<n + m> cc;
         cc.init(S.Cpk, T, B, b);
         win = ilqr_problem<Model, BM, TRAJ_REC, true, CostDiagConst<n + m>, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd,
-                                                      decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
-                                                      alpha, b_lds, S.cost);
+                                                      decay, max_ls, gr, xsa, nullptr, xsb, nullptr, du_sq, cost,
+                                                      alpha, b_lds, prev_cost);
       } else {
         __builtin_unreachable();
       }
@@ -737,35 +735,70 @@ __global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const floa
       if constexpr (packed_diag_ok<n + m>())
         win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m, true>, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr,
                                                       nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb,
-                                                      nullptr, S.du_sq, cost, alpha, b_lds, S.cost);
+                                                      nullptr, du_sq, cost, alpha, b_lds, prev_cost);
       else
         __builtin_unreachable();
     } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
       win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m, false, true>, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T},
                                                     nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr,
-                                                    xsb, nullptr, S.du_sq, cost, alpha, b_lds, S.cost);
+                                                    xsb, nullptr, du_sq, cost, alpha, b_lds, prev_cost);
     else if (pk & kCostSym)
       win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m>, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
                                                     xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
-                                                    S.du_sq, cost, alpha, b_lds, S.cost);
+                                                    du_sq, cost, alpha, b_lds, prev_cost);
     else
       win = ilqr_problem<Model, BM, TRAJ_REC, true, CostFull<n + m>, true>(T, B, b, md, x_init, full, nullptr, nullptr, xcur, nullptr, bd,
-                                                    decay, max_ls, gr, xsa, nullptr, xsb, nullptr, S.du_sq, cost,
-                                                    alpha, b_lds, S.cost);
+                                                    decay, max_ls, gr, xsa, nullptr, xsb, nullptr, du_sq, cost,
+                                                    alpha, b_lds, prev_cost);
 #endif
   }
+  return LaneIter{cost, alpha, win ? sb : sa};
+}
+
+// best-iterate test (mpc_explicit.py:277-283): iteration 0 always takes it
+DEV bool mpc_takes_best(bool first, float cost, float best_cost, float best_cost_eps) {
+  return first || cost <= best_cost + best_cost_eps;
+}
+
+// One launch per MPC iteration (the stop-rule path; fixed-count solves of the
+// single-lane models run k_mpc_solve_fixed instead).  FIRST: iteration 0 — its
+// own instantiation, so the steady-state kernel carries no copy-building code
+// and profiles separately.
+template <class Model, int BM, bool LG, bool FIRST>
+__global__ void __launch_bounds__(kBlock) k_mpc_iterate(int T, int B, const float* __restrict__ theta,
+                                                        const float* __restrict__ x_init, const float* __restrict__ C,
+                                                        const float* __restrict__ c, Bounds bd, float decay, int max_ls,
+                                                        int iteration, float best_cost_eps, float eps,
+                                                        int not_improved_lim, int G, MpcState S) {
+  constexpr bool first = FIRST;                             // == (iteration == 0), chosen by the host
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  // the problem's slot indices, cost flags and costs are read together with the
+  // stop rule's inputs (one memory latency in the prologue, not several)
+  const int bl = b < B ? b : B - 1;
+  const int cur = S.slot[bl], best = S.slot[B + bl];
+  const unsigned char pk = (!FIRST && S.Cpk) ? S.cost_sym[bl] : 0;
+  const float prev = FIRST ? 0.f : S.cost[bl];
+  const float best_cost = FIRST ? 0.f : S.best_cost[bl];
+  DILQR_STAMP(0);
+  DILQR_STAMP(6);
+  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
+  if (b >= B) return;
+  DILQR_STAMP(1);
+  Model md; md.load(theta);
+  extern __shared__ __attribute__((aligned(16))) float lds_gains[];
+  const LaneIter r = mpc_iteration_lane<Model, BM, LG, FIRST>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
+                                                              S.du_sq, lds_gains, cur, best, pk, prev);
   DILQR_STAMP(3);
-  const int nw = win ? sb : sa;
-  S.cost[b] = cost;
-  S.alpha[b] = alpha;
-  bool better = !first && (cost <= S.best_cost[b] + best_cost_eps);      // mpc_explicit.py:278
-  if (first || better) {
-    S.best_cost[b] = cost;
-    S.slot[B + b] = (unsigned char)nw;
+  S.cost[b] = r.cost;
+  S.alpha[b] = r.alpha;
+  const bool take = mpc_takes_best(first, r.cost, best_cost, best_cost_eps);
+  if (take) {
+    S.best_cost[b] = r.cost;
+    S.slot[B + b] = (unsigned char)r.slot;
   }
-  S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
-  if (S.best_iter && (first || better)) S.best_iter[b] = iteration;       // fixed-count solves
-  S.slot[b] = (unsigned char)nw;
+  S.improved[b] = take ? (first ? 1 : 2) : 0;
+  if (S.best_iter && take) S.best_iter[b] = iteration;      // fixed-count solves
+  S.slot[b] = (unsigned char)r.slot;
   DILQR_STAMP(4);
   DILQR_STAMP(7);
 }
@@ -863,6 +896,94 @@ template <class Model>
 constexpr int slot_layout() { return Model::N + Model::M <= 8 ? TRAJ_REC : TRAJ_AOS; }
 constexpr int slot_layout_nm(int n, int m) { return n + m <= 8 ? TRAJ_REC : TRAJ_AOS; }
 
+// get_traj(u_init) of problem b into slot 0 (util.py:104-127; u_init: the
+// caller's [T,B,m] controls, or null for zeros, the MPC default) and its slot
+// indices reset; the states and controls are written in one pass.
+template <class Model>
+DEV void mpc_begin_lane(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
+                        const float* __restrict__ u_init, const MpcState& S) {
+  constexpr int n = Model::N, m = Model::M;
+  S.slot[b] = 0; S.slot[B + b] = 0;
+  constexpr int TL = slot_layout<Model>();
+  float xt[n];
+  ld(xt, x_init + (size_t)b * n);
+  for (int t = 0; t < T; ++t) {
+    float ut[m], xn[n];
+    if (u_init) {
+      ld(ut, u_init + ((size_t)t * B + b) * m);
+    } else {
+#pragma unroll
+      for (int a = 0; a < m; ++a) ut[a] = 0.f;
+    }
+    st_xu<TL>(S.Xs, S.Us, xt, ut, t, B, b);
+    if (t < T - 1) {
+      md.forward(xt, ut, xn);
+#pragma unroll
+      for (int i = 0; i < n; ++i) xt[i] = xn[i];
+    }
+  }
+}
+
+// The control words and the stop rule's sync counters of a new solve.
+DEV void mpc_reset_ctrl(const MpcState& S) {
+  dilqr_mpc_ctrl z = {};
+  S.ctrl[0] = z;
+  S.ctrl[1] = z;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) S.done_counter[i] = 0u;
+}
+
+// ---------------- a whole fixed-count solve in ONE launch (thread-per-problem
+// models).  With eps <= 0 and not_improved_lim >= the iteration count the stop
+// rule cannot fire (mpc_explicit.py:297-299), so nothing couples two problems
+// until the final best_du (k_mpc_fixed_finish, whose quirk rows mix the batch):
+// each lane runs begin, iteration 0 and iterations 1..iters-1 of its problem
+// back to back — the same per-lane code as k_mpc_begin + k_mpc_iterate<FIRST>
+// + k_mpc_iterate<steady>, so the same bits — holding its slot indices, cost
+// flags and costs in registers between iterations.  What this saves is the
+// per-launch cost at one wave per SIMD: dispatch, ramp and the wait for the
+// grid's slowest wave, once per iteration.  A lane reads back
+// only trajectory records it wrote itself, and the gain records in LDS are its
+// own, so no barrier is involved; every lane's loop runs exactly `iters`
+// iterations and exits.
+template <class Model, int BM, bool LG>
+__global__ void __launch_bounds__(kBlock) k_mpc_solve_fixed(int T, int B, const float* __restrict__ theta,
+                                                            const float* __restrict__ x_init,
+                                                            const float* __restrict__ u_init,
+                                                            const float* __restrict__ C, const float* __restrict__ c,
+                                                            Bounds bd, float decay, int max_ls, int iters,
+                                                            float best_cost_eps, MpcState S) {
+  constexpr int m = Model::M;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b == 0) mpc_reset_ctrl(S);
+  if (b >= B) return;
+  Model md; md.load(theta);
+  extern __shared__ __attribute__((aligned(16))) float lds_gains[];
+  mpc_begin_lane<Model>(T, B, b, md, x_init, u_init, S);
+  unsigned pk = 0;
+  LaneIter r = mpc_iteration_lane<Model, BM, LG, true>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S, S.du_sq,
+                                                       lds_gains, 0, 0, 0u, 0.f, &pk);
+  int cur = r.slot, best = r.slot, best_iter = 0;
+  float best_cost = r.cost;
+  bool take = true;
+  const size_t plane = (size_t)T * m * B;                   // one iteration's du rows
+  for (int it = 1; it < iters; ++it) {
+    r = mpc_iteration_lane<Model, BM, LG, false>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
+                                                 S.du_sq + it * plane, lds_gains, cur, best, pk, r.cost);
+    take = mpc_takes_best(false, r.cost, best_cost, best_cost_eps);
+    if (take) { best_cost = r.cost; best = r.slot; best_iter = it; }
+    cur = r.slot;
+  }
+  // the state the per-iteration launches leave behind
+  S.cost[b] = r.cost;
+  S.alpha[b] = r.alpha;
+  S.best_cost[b] = best_cost;
+  S.slot[b] = (unsigned char)cur;
+  S.slot[B + b] = (unsigned char)best;
+  S.improved[b] = take ? (iters == 1 ? 1 : 2) : 0;
+  S.best_iter[b] = best_iter;
+}
+
 // ---------------------------------------------------------------- launchers
 // the fused MPC iteration of one thread-per-problem model: bounds mode, gain
 // records in LDS when four workgroups per CU still fit, iteration 0's own
@@ -887,6 +1008,26 @@ int launch_mpc_step_tpp(const MpcStepArgs& a) {
   else LAUNCH_MPC(DILQR_BOUNDS_NONE);
 #undef LAUNCH_MPC
 #undef LAUNCH_IT
+  return launched();
+}
+
+// a whole fixed-count solve of one thread-per-problem model (k_mpc_solve_fixed)
+template <class MD>
+int launch_mpc_solve_tpp(const MpcSolveArgs& a) {
+#define LAUNCH_SOLVE(BM_)                                                                                    \
+  do {                                                                                                       \
+    const size_t lds = (size_t)a.T * kBlock * (MD::N * MD::M + MD::M) * sizeof(float);                      \
+    if (lds * 4 <= kLdsPerCU && !kNoLdsGains)                                                                \
+      k_mpc_solve_fixed<MD, BM_, true><<<grid_for(a.B), kBlock, lds, a.stream>>>(                             \
+          a.T, a.B, a.theta, a.x_init, a.u_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iters, a.best_cost_eps, a.st); \
+    else                                                                                                     \
+      k_mpc_solve_fixed<MD, BM_, false><<<grid_for(a.B), kBlock, 0, a.stream>>>(                              \
+          a.T, a.B, a.theta, a.x_init, a.u_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iters, a.best_cost_eps, a.st); \
+  } while (0)
+  if (a.bd.mode == DILQR_BOUNDS_TENSOR) LAUNCH_SOLVE(DILQR_BOUNDS_TENSOR);
+  else if (a.bd.mode != DILQR_BOUNDS_NONE) LAUNCH_SOLVE(DILQR_BOUNDS_SCALAR);
+  else LAUNCH_SOLVE(DILQR_BOUNDS_NONE);
+#undef LAUNCH_SOLVE
   return launched();
 }
 

@@ -22,6 +22,19 @@ struct MpcStepArgs {
   hipStream_t stream;
 };
 
+// A whole fixed-count solve in one launch (dilqr_mpc_solve_fixed_f32; the
+// thread-per-problem models).
+struct MpcSolveArgs {
+  int T, B;
+  const float *theta, *x_init, *u_init, *C, *c;
+  Bounds bd;
+  float decay;
+  int max_ls, iters;
+  float best_cost_eps;
+  dilqr_mpc_state st;
+  hipStream_t stream;
+};
+
 // One standalone fused iteration (dilqr_ilqr_iterate_f32).
 struct IlqrIterArgs {
   int T, B;
@@ -37,6 +50,8 @@ struct IlqrIterArgs {
 int launch_mpc_step_pendulum(const MpcStepArgs& a);
 int launch_mpc_step_cartpole(const MpcStepArgs& a);
 int launch_mpc_step_rocket(const MpcStepArgs& a);
+int launch_mpc_solve_pendulum(const MpcSolveArgs& a);
+int launch_mpc_solve_cartpole(const MpcSolveArgs& a);
 int launch_ilqr_iterate_pendulum(const IlqrIterArgs& a);
 int launch_ilqr_iterate_cartpole(const IlqrIterArgs& a);
 int launch_ilqr_iterate_rocket(const IlqrIterArgs& a);

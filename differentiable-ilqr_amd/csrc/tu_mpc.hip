@@ -121,43 +121,17 @@ __global__ void __launch_bounds__(256) k_mpc_fixed_finish(int TM, int B, int ite
   }
 }
 
-// rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl.
-// u_init: the caller's [T,B,m] controls, or null for zeros (the MPC default):
-// read once, written into the slot with the states in the same pass.
+// rollout of u_init into slot 0 (util.get_traj) + reset of slots/ctrl
+// (mpc_begin_lane; u_init null: zeros, the MPC default).
 template <class Model>
 __global__ void __launch_bounds__(kBlock) k_mpc_begin(int T, int B, const float* __restrict__ theta,
                                                       const float* __restrict__ x_init,
                                                       const float* __restrict__ u_init, MpcState S) {
-  constexpr int n = Model::N, m = Model::M;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b == 0) {
-    dilqr_mpc_ctrl z = {};
-    S.ctrl[0] = z;
-    S.ctrl[1] = z;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) S.done_counter[i] = 0u;
-  }
+  if (b == 0) mpc_reset_ctrl(S);
   if (b >= B) return;
   Model md; md.load(theta);
-  S.slot[b] = 0; S.slot[B + b] = 0;
-  constexpr int TL = slot_layout<Model>();
-  float xt[n];
-  ld(xt, x_init + (size_t)b * n);
-  for (int t = 0; t < T; ++t) {
-    float ut[m], xn[n];
-    if (u_init) {
-      ld(ut, u_init + ((size_t)t * B + b) * m);
-    } else {
-#pragma unroll
-      for (int a = 0; a < m; ++a) ut[a] = 0.f;
-    }
-    st_xu<TL>(S.Xs, S.Us, xt, ut, t, B, b);
-    if (t < T - 1) {
-      md.forward(xt, ut, xn);
-#pragma unroll
-      for (int i = 0; i < n; ++i) xt[i] = xn[i];
-    }
-  }
+  mpc_begin_lane<Model>(T, B, b, md, x_init, u_init, S);
 }
 
 template <int n, int m>
@@ -357,6 +331,34 @@ int dilqr_mpc_finish_fixed_f32(int T, int m, int B, int iterations, dilqr_mpc_st
   if (B == 0) return 0;
   k_mpc_fixed_finish<<<(B + 255) / 256, 256, 0, S(stream)>>>(T * m, B, iterations, st);
   return launched();
+}
+
+int dilqr_mpc_solve_fixed_f32(int model, int T, int B, const float* theta, const float* x_init, const float* u_init,
+                              const float* C, const float* c, dilqr_bounds bounds, float linesearch_decay,
+                              int max_linesearch_iter, int iterations, float best_cost_eps, dilqr_mpc_state st,
+                              void* stream) {
+  if (T < 1 || B < 0 || max_linesearch_iter < 1 || iterations < 1 || !theta || !x_init || !C || !c) return DILQR_E_ARG;
+  if (!al16(x_init) || !al16(C) || !al16(c) || bad_state(st) || bad_bounds(bounds) || !st.best_iter)
+    return DILQR_E_ARG;
+  if (u_init && ((uintptr_t)u_init & 3u)) return DILQR_E_ARG;
+  const int m = dilqr_model_num_ctrl(model);
+  if (m < 1) return DILQR_E_SHAPE;
+  if (B == 0) return 0;
+  int e;
+  if (model == DILQR_MODEL_PENDULUM || model == DILQR_MODEL_CARTPOLE) {
+    const MpcSolveArgs a{T, B, theta, x_init, u_init, C, c, mkb(bounds), linesearch_decay, max_linesearch_iter,
+                         iterations, best_cost_eps, st, S(stream)};
+    e = model == DILQR_MODEL_CARTPOLE ? launch_mpc_solve_cartpole(a) : launch_mpc_solve_pendulum(a);
+  } else {
+    // the 16-lanes-per-problem models change their lane mapping between the
+    // sweep and the line search: one launch pair per iteration
+    e = dilqr_mpc_begin_f32(model, T, B, theta, x_init, u_init, st, stream);
+    for (int i = 0; !e && i < iterations; ++i)
+      e = dilqr_mpc_iterate_fixed_f32(model, T, B, theta, x_init, C, c, bounds, linesearch_decay,
+                                      max_linesearch_iter, i, best_cost_eps, st, stream);
+  }
+  if (e) return e;
+  return dilqr_mpc_finish_fixed_f32(T, m, B, iterations, st, stream);
 }
 
 int dilqr_mpc_stop_rule_f32(int T, int m, int B, int iteration, dilqr_mpc_state st, void* stream) {

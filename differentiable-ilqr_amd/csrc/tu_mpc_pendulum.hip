@@ -5,4 +5,5 @@
 namespace dilqr {
 int launch_mpc_step_pendulum(const MpcStepArgs& a) { return launch_mpc_step_tpp<Pendulum>(a); }
 int launch_ilqr_iterate_pendulum(const IlqrIterArgs& a) { return launch_ilqr_iterate_tpp<Pendulum>(a); }
+int launch_mpc_solve_pendulum(const MpcSolveArgs& a) { return launch_mpc_solve_tpp<Pendulum>(a); }
 }  // namespace dilqr

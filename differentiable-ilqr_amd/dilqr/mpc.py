@@ -73,14 +73,24 @@ class MPC(Module):
             Fd = dx.F.detach().contiguous()
             fd = None if (dx.f is None or dx.f.nelement() == 0) else dx.f.detach().contiguous()
         with torch.no_grad():
-            ws = ops.mpc_solve_unfused(model_id, theta, x_init.detach(), C.detach().contiguous(),
-                                       c.detach().contiguous(), T, F=Fd, f=fd, u_init=self.u_init,
-                                       u_lower=self.u_lower, u_upper=self.u_upper, lqr_iter=self.lqr_iter,
-                                       eps=self.eps, linesearch_decay=self.linesearch_decay,
-                                       max_linesearch_iter=self.max_linesearch_iter,
-                                       not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps,
-                                       u_zero_I=self.u_zero_I)
-        x, u, costs, full_du_norm = ws.best_x, ws.best_u, ws.best_cost, ws.best_du
+            if not lin and self.u_zero_I is None:
+                # an env_dx model: the device-resident fused loop (its iterates equal
+                # the unfused pipeline's bit for bit, test_fused_iteration_equals_unfused)
+                x, u, costs, full_du_norm, _sv = ops.mpc_solve(
+                    model_id, theta, x_init.detach(), C.detach().contiguous(), c.detach().contiguous(), T,
+                    u_init=self.u_init, u_lower=self.u_lower, u_upper=self.u_upper, lqr_iter=self.lqr_iter,
+                    eps=self.eps, linesearch_decay=self.linesearch_decay,
+                    max_linesearch_iter=self.max_linesearch_iter, not_improved_lim=self.not_improved_lim,
+                    best_cost_eps=self.best_cost_eps)
+            else:
+                ws = ops.mpc_solve_unfused(model_id, theta, x_init.detach(), C.detach().contiguous(),
+                                           c.detach().contiguous(), T, F=Fd, f=fd, u_init=self.u_init,
+                                           u_lower=self.u_lower, u_upper=self.u_upper, lqr_iter=self.lqr_iter,
+                                           eps=self.eps, linesearch_decay=self.linesearch_decay,
+                                           max_linesearch_iter=self.max_linesearch_iter,
+                                           not_improved_lim=self.not_improved_lim,
+                                           best_cost_eps=self.best_cost_eps, u_zero_I=self.u_zero_I)
+                x, u, costs, full_du_norm = ws.best_x, ws.best_u, ws.best_cost, ws.best_du
         if torch.is_grad_enabled() and self.backprop:
             if lin:
                 F, f = dx.F, (dx.f if dx.f is not None else torch.empty(0, device=x.device))

@@ -234,20 +234,38 @@ class MPCSolve:
             self.du_sq, self.full_du_norm, self.ws, self.ctrl, self.counter, self.Cpk, self.cost_sym,
             self.best_iter)])
 
+    def _u_init(self, u_init):
+        if u_init is None:
+            return None
+        u0 = u_init.to(device=self.Xs.device, dtype=torch.float32)
+        if u0.ndimension() == 2:
+            u0 = u0.unsqueeze(1).expand(self.T, self.B, self.m)
+        u0 = u0.contiguous()
+        if tuple(u0.shape) != (self.T, self.B, self.m):
+            raise ValueError(f"u_init: expected [T, B, m] = {(self.T, self.B, self.m)} or [T, m], got "
+                             f"{tuple(u_init.shape)}")
+        return u0
+
     def begin(self, model_id, theta, x_init, u_init=None):
         """x = get_traj(u_init or 0) into slot 0; reset slots and the control block."""
-        u0 = None
-        if u_init is not None:
-            u0 = u_init.to(device=self.Xs.device, dtype=torch.float32)
-            if u0.ndimension() == 2:
-                u0 = u0.unsqueeze(1).expand(self.T, self.B, self.m)
-            u0 = u0.contiguous()
-            if tuple(u0.shape) != (self.T, self.B, self.m):
-                raise ValueError(f"u_init: expected [T, B, m] = {(self.T, self.B, self.m)} or [T, m], got "
-                                 f"{tuple(u_init.shape)}")
+        u0 = self._u_init(u_init)
         N.call("dilqr_mpc_begin_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init),
                None if u0 is None else N.ptr(u0), self.state, N.stream(x_init.device))
         self._u0 = u0                       # alive until the launch has read it
+
+    def solve_fixed(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, best_cost_eps, u_init=None):
+        """A whole fixed-count solve of fixed_iters iterations in one call
+        (dilqr_mpc_solve_fixed_f32: begin + every iteration in one launch for
+        the single-lane models, then finish); the same bits as begin +
+        iterate_fixed per iteration + finish_fixed."""
+        if not self.fixed_iters:
+            raise ValueError("solve_fixed: solve not built for a fixed count")
+        u0 = self._u_init(u_init)
+        N.call("dilqr_mpc_solve_fixed_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init),
+               None if u0 is None else N.ptr(u0), N.ptr(C), N.ptr(c), bounds, float(decay), int(max_ls),
+               int(self.fixed_iters), float(best_cost_eps), self.state, N.stream(x_init.device))
+        self._u0 = u0
+        self.last_iteration = self.fixed_iters - 1
 
     def iterate(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, iteration, best_cost_eps, eps,
                 not_improved_lim):
@@ -313,16 +331,14 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     fixed = (lqr_iter >= 1 and eps <= 0 and not_improved_lim >= lqr_iter
              and plane_bytes <= min(2 ** 31, torch.cuda.mem_get_info(x_init.device)[0] // 16))
     sv = MPCSolve(T, B, n, m, x_init.device, fixed_iters=lqr_iter if fixed else None)
-    sv.begin(model_id, theta, x_init, u_init)
     bounds, keep = N.make_bounds(u_lower, u_upper)
     if fixed:
-        for i in range(lqr_iter):
-            sv.iterate_fixed(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i,
-                             best_cost_eps)
-        sv.finish_fixed(lqr_iter)
+        sv.solve_fixed(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, best_cost_eps,
+                       u_init)
         del keep
         x, u = sv.gather_best()
         return x, u, sv.best_cost, sv.best_du, sv
+    sv.begin(model_id, theta, x_init, u_init)
     for i in range(lqr_iter):
         sv.iterate(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i,
                    best_cost_eps, eps, not_improved_lim)
@@ -404,8 +420,10 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
         del keep
         ws.xa, ws.xb = ws.xb, ws.xa
         ws.ua, ws.ub = ws.ub, ws.ua
-        # a stopped loop must not keep iterating: the unfused kernels have no
-        # device-side guard, so poll every iteration here.
-        if int(ws.ctrl[1].item()):
+        # once the stop rule fired, k_mpc_best ignores further iterations (the
+        # best iterate, its cost, best_du and the control word stay as they
+        # were), so the loop can run on past the stop: the host polls the flag
+        # only every check_every iterations, like mpc_solve
+        if check_every and (i + 1) % check_every == 0 and i + 1 < lqr_iter and int(ws.ctrl[1].item()):
             break
     return ws

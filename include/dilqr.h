@@ -61,7 +61,7 @@ typedef struct dilqr_bounds {
   const float* hi_t;             /* [T,B,m] or NULL                              */
 } dilqr_bounds;
 
-/* Library version (for the loader's sanity check): 5. */
+/* Library version (for the loader's sanity check): 6. */
 int dilqr_version(void);
 
 /* Build id: the first 16 hex digits of the sha256 of the sources the library
@@ -340,6 +340,20 @@ int dilqr_mpc_iterate_fixed_f32(int model, int T, int B, const float* theta, con
                                 float best_cost_eps, dilqr_mpc_state st, void* stream);
 int dilqr_mpc_finish_fixed_f32(int T, int m, int B, int iterations, dilqr_mpc_state st,
                                void* stream);
+
+/* A whole fixed-count solve in one call (ABI 6): begin (u_init as in
+   dilqr_mpc_begin_f32), `iterations` iterations, finish — the same results,
+   bit for bit, as dilqr_mpc_begin_f32 + dilqr_mpc_iterate_fixed_f32 per
+   iteration + dilqr_mpc_finish_fixed_f32.  Pendulum and cartpole run begin
+   and every iteration in ONE launch (each lane iterates its own problem; no
+   problem couples to another until best_du), then the finish launch; rocket
+   keeps its per-iteration launch pairs.  st.du_sq must hold iterations*T*m*B
+   floats and st.best_iter must be set. */
+int dilqr_mpc_solve_fixed_f32(int model, int T, int B, const float* theta, const float* x_init,
+                              const float* u_init, const float* C, const float* c,
+                              dilqr_bounds bounds, float linesearch_decay,
+                              int max_linesearch_iter, int iterations, float best_cost_eps,
+                              dilqr_mpc_state st, void* stream);
 
 /* Materialise each problem's best trajectory into x_out [T,B,n], u_out [T,B,m]. */
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out,

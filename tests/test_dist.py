@@ -86,7 +86,7 @@ def test_bench_sharded_hip_path_equals_whole_batch(tmp_path):
     env = dict(os.environ, BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-           "--gpus", str(world), "--batch", str(B_per), "--steps", str(it), "--warmup", "0", "--lqr-iter", str(it),
+           "--gpus", str(world), "--batch", str(B_per), "--steps", "2", "--warmup", "0", "--lqr-iter", str(it),
            "--no-secondary", "--no-cpu-baseline", "--dump", str(tmp_path)]
     r = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -494,6 +494,43 @@ def test_fixed_count_solve_equals_stop_rule_path(golden, name):
     assert torch.equal(a.full_du_norm, sv.full_du_norm)
 
 
+@pytest.mark.parametrize("name,warm", [("cart_unc", False), ("cart_box10", True), ("pend_box", False),
+                                       ("pend_unc", True), ("rocket_unc", False)])
+def test_whole_solve_launch_equals_per_iteration_launches(golden, name, warm):
+    """dilqr_mpc_solve_fixed_f32 (begin + every iteration in ONE launch for the
+    single-lane models, each lane iterating its own problem) leaves exactly the
+    state of begin + one iterate_fixed launch per iteration + finish_fixed:
+    slots, costs, step sizes, improved flags, best iterate, best_iter, best_du,
+    full_du_norm — bit for bit, with and without a warm start u_init."""
+    from dilqr import _native as N
+    from dilqr import ops
+    g = golden("mpc_f64")
+    mname, T, it, bounds, _eps, _nil, decay, mls = MPC_CASES[name]
+    dx = dilqr_models()[mname]()
+    x0 = gpu(g[f"{name}_x0"])
+    B, n, m = x0.shape[0], dx.n_state, dx.n_ctrl
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV).contiguous()
+    c = p.repeat(T, B, 1).to(DEV).contiguous()
+    theta = ops.theta_of(dx, x0)
+    lo, hi = bounds if bounds else (None, None)
+    bd, _keep = N.make_bounds(lo, hi)
+    u0 = 0.3 * torch.randn(T, B, m, generator=torch.Generator().manual_seed(5)).to(DEV) if warm else None
+    a = ops.MPCSolve(T, B, n, m, x0.device, fixed_iters=it)
+    a.begin(dx.model_id, theta, x0, u0)
+    for i in range(it):
+        a.iterate_fixed(dx.model_id, theta, x0, C, c, bd, decay, mls, i, 1e-4)
+    a.finish_fixed(it)
+    b = ops.MPCSolve(T, B, n, m, x0.device, fixed_iters=it)
+    b.solve_fixed(dx.model_id, theta, x0, C, c, bd, decay, mls, 1e-4, u0)
+    for key in ("slot", "cost", "alpha", "improved", "best_cost", "best_du", "full_du_norm", "best_iter"):
+        assert same_bits(getattr(a, key).float(), getattr(b, key).float()), key
+    xa, ua = a.gather_best()
+    xb, ub = b.gather_best()
+    assert torch.equal(xa, xb) and torch.equal(ua, ub)
+    assert a.iterations == b.iterations == it
+
+
 # ------------------------------------------------------------------ DiLQR implicit backward
 IMPLICIT = {"cart_unc": ("cartpole", None), "cart_box": ("cartpole", (-5.0, 5.0)),
             "pend_box": ("pendulum", (-2.0, 2.0)), "rock_unc": ("rocket", None),
