@@ -317,7 +317,10 @@ constexpr int kPFL = DILQR_PF_LS;                   // the line search's prefetc
 // and B), sharing every load of the step; the first accepted candidate wins,
 // which is exactly the sequential search.  A wave otherwise pays a whole
 // second latency-bound pass whenever any of its 64 problems backtracks.
-template <class Model, int BM, int TL, class CostT>
+// PAIR: the common MPC case as its own instantiation — exactly one round of two
+// candidates (max_ls == 2) with B's records in the gain slots — so the step
+// loop carries no test of the round, of "is there a B", of "where does B go".
+template <class Model, int BM, int TL, class CostT, bool PAIR = false>
 DEV int line_search(int T, int B, int b, const Model md, const float* __restrict__ x_init, const CostT& cs,
                     const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd, float decay,
                     int max_ls, const GainRecs& ws, float* __restrict__ xa_out,
@@ -331,6 +334,10 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
   // floats), and only the problems whose B wins copy it to xb_out at the end —
   // instead of every problem writing both candidates to HBM.
   static_assert(TL != TRAJ_REC || GREC == d, "B records in the gain slots need m = 1");
+  if constexpr (PAIR) {
+    max_ls = 2;
+    b_in_gains = true;
+  }
   float alpha = 1.f, cost = 0.f;
   int win = 0;
   // Candidates A and B travel as the two components of f2 values: every
@@ -605,10 +612,18 @@ DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restric
     if (pack_out && sym && diag && tinv) {              // iteration 0 of a diag(q), p over t cost
       CostDiagConst<d> cc;
       cc.set(pk_last);
+      if (b_in_gains && max_ls == 2)
+        return line_search<Model, BM, TL, CostDiagConst<d>, true>(T, B, b, md, x_init, cc, x, u, bd, decay, max_ls, ws,
+                                                                  xa_out, ua_out, xb_out, ub_out, du_sq, old_cost,
+                                                                  cost_out, alpha_out, b_in_gains);
       return line_search<Model, BM, TL>(T, B, b, md, x_init, cc, x, u, bd, decay, max_ls, ws, xa_out, ua_out,
                                          xb_out, ub_out, du_sq, old_cost, cost_out, alpha_out, b_in_gains);
     }
   }
+  if (b_in_gains && max_ls == 2)
+    return line_search<Model, BM, TL, CostT, true>(T, B, b, md, x_init, cs, x, u, bd, decay, max_ls, ws, xa_out,
+                                                   ua_out, xb_out, ub_out, du_sq, old_cost, cost_out, alpha_out,
+                                                   b_in_gains);
   return line_search<Model, BM, TL>(T, B, b, md, x_init, cs, x, u, bd, decay, max_ls, ws, xa_out, ua_out, xb_out,
                                      ub_out, du_sq, old_cost, cost_out, alpha_out, b_in_gains);
 }
@@ -955,19 +970,26 @@ __global__ void __launch_bounds__(kBlock) k_mpc_solve_fixed(int T, int B, const 
                                                             float best_cost_eps, MpcState S) {
   constexpr int m = Model::M;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  // diagnostic stamps (tools/phase_stamps.py solve): 0/6 entry, 1 begin done,
+  // 3 iteration 0 done, 4 last iteration starts, 2 its sweep done, 5/7 exit
+  DILQR_STAMP(0);
+  DILQR_STAMP(6);
   if (b == 0) mpc_reset_ctrl(S);
   if (b >= B) return;
   Model md; md.load(theta);
   extern __shared__ __attribute__((aligned(16))) float lds_gains[];
   mpc_begin_lane<Model>(T, B, b, md, x_init, u_init, S);
+  DILQR_STAMP(1);
   unsigned pk = 0;
   LaneIter r = mpc_iteration_lane<Model, BM, LG, true>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S, S.du_sq,
                                                        lds_gains, 0, 0, 0u, 0.f, &pk);
   int cur = r.slot, best = r.slot, best_iter = 0;
   float best_cost = r.cost;
   bool take = true;
+  DILQR_STAMP(3);
   const size_t plane = (size_t)T * m * B;                   // one iteration's du rows
   for (int it = 1; it < iters; ++it) {
+    if (it == iters - 1) DILQR_STAMP(4);
     r = mpc_iteration_lane<Model, BM, LG, false>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
                                                  S.du_sq + it * plane, lds_gains, cur, best, pk, r.cost);
     take = mpc_takes_best(false, r.cost, best_cost, best_cost_eps);
@@ -982,6 +1004,8 @@ __global__ void __launch_bounds__(kBlock) k_mpc_solve_fixed(int T, int B, const 
   S.slot[B + b] = (unsigned char)best;
   S.improved[b] = take ? (iters == 1 ? 1 : 2) : 0;
   S.best_iter[b] = best_iter;
+  DILQR_STAMP(5);
+  DILQR_STAMP(7);
 }
 
 // ---------------------------------------------------------------- launchers

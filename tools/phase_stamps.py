@@ -9,6 +9,7 @@ old cost), line search, epilogue.  The clock is s_memtime / s_memrealtime
   make -C differentiable-ilqr_amd stamps      # here, on the CPU
   python tools/phase_stamps.py [iteration]     # on the GPU box
   BOUNDS=100 python tools/phase_stamps.py       # config 4 (box +-100)
+  python tools/phase_stamps.py solve           # the whole-solve launch (k_mpc_solve_fixed)
 """
 import ctypes
 import json
@@ -29,7 +30,8 @@ from dilqr import ops  # noqa: E402
 dev = torch.device("cuda", 0)
 T, n, m = bench.T_HORIZON, bench.N_STATE, bench.N_CTRL
 B = bench.B_PER_GPU
-STOP_AT = int(sys.argv[1]) if len(sys.argv) > 1 else 5         # stamps of this iteration
+SOLVE = len(sys.argv) > 1 and sys.argv[1] == "solve"
+STOP_AT = int(sys.argv[1]) if len(sys.argv) > 1 and not SOLVE else 5         # stamps of this iteration
 x0n, q, p = bench.make_problems(B)
 x0 = torch.tensor(x0n, device=dev)
 C = torch.diag(torch.tensor(q)).repeat(T, B, 1, 1).to(dev).contiguous()
@@ -45,6 +47,30 @@ lib.dilqr_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 lib.dilqr_debug_stamps.restype = ctypes.c_int
 
 rows = []
+if SOLVE:
+    ITERS = 10
+    sv = ops.MPCSolve(T, B, n, m, dev, fixed_iters=ITERS)
+    for solve in range(4):
+        sv.solve_fixed(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, 1e-4)
+        torch.cuda.synchronize()
+        buf = np.zeros(W * 8, dtype=np.uint64)
+        assert lib.dilqr_debug_stamps(buf.ctypes.data, W * 8) == 0
+        rows.append(buf.reshape(W, 8).astype(np.int64))
+    out = {"kernel": "k_mpc_solve_fixed", "iterations": ITERS, "waves": W, "bounds": LIM or None}
+    r = rows[-1]
+    ghz = (r[:, 5] - r[:, 0]) / ((r[:, 7] - r[:, 6]) / 100e6) / 1e9
+    out["clock_ghz_median"] = float(np.median(ghz))
+    for name, a, b_, div in (("begin", 0, 1, 1), ("iteration0", 1, 3, 1), ("steady_iteration", 3, 4, ITERS - 2),
+                             ("last_sweep", 4, 2, 1), ("last_line_search", 2, 5, 1), ("wave", 0, 5, 1)):
+        cyc = np.concatenate([(x[:, b_] - x[:, a]) / div for x in rows[1:]])
+        out[name + "_cycles"] = {"median": float(np.median(cyc)), "p10": float(np.percentile(cyc, 10)),
+                                 "p90": float(np.percentile(cyc, 90)), "max": float(cyc.max())}
+        out[name + "_us_median"] = float(np.median(cyc) / (out["clock_ghz_median"] * 1e3))
+    out["kernel_span_us"] = float(np.median([(x[:, 7].max() - x[:, 6].min()) / 100.0 for x in rows[1:]]))
+    out["wave_end_spread_us"] = float(np.median([(x[:, 7].max() - x[:, 7].min()) / 100.0 for x in rows[1:]]))
+    out["wave_start_spread_us"] = float(np.median([(x[:, 6].max() - x[:, 6].min()) / 100.0 for x in rows[1:]]))
+    print(json.dumps(out))
+    sys.exit(0)
 for solve in range(4):
     sv.begin(N.MODEL_CARTPOLE, theta, x0)
     for i in range(STOP_AT + 1):
