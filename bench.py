@@ -255,14 +255,15 @@ def with_pmc(entry, sig):
         ks = [pmc.get(s_) for s_ in sig]
         if all(ks):
             entry["traffic"] = sum(k.get("hbm_bytes_per_launch", 0.0) for k in ks)
-            entry["pmc"] = {s_: {f: v for f, v in k.items() if f != "hbm_bytes_per_launch"} for s_, k in zip(sig, ks)}
-            entry["pmc_measured_at"] = PMC_COMMIT[0]
+            entry["pmc"] = {s_: {f: v for f, v in k.items() if f not in ("hbm_bytes_per_launch", "measured_at")}
+                            for s_, k in zip(sig, ks)}
+            entry["pmc_measured_at"] = ks[0].get("measured_at", PMC_COMMIT[0])
         return entry
     k = pmc.get(sig)
     if k:
         entry["traffic"] = k.get("hbm_bytes_per_launch")
-        entry["pmc"] = {f: v for f, v in k.items() if f != "hbm_bytes_per_launch"}
-        entry["pmc_measured_at"] = PMC_COMMIT[0]
+        entry["pmc"] = {f: v for f, v in k.items() if f not in ("hbm_bytes_per_launch", "measured_at")}
+        entry["pmc_measured_at"] = k.get("measured_at", PMC_COMMIT[0])
     return entry
 
 
@@ -678,17 +679,19 @@ def main():
                                    f"{args.lqr_iter - 1} steady iterations; " + cost_path + ")",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_measured_at": PMC_COMMIT[0],
+                         "traffic_measured_at": head_pmc.get("measured_at", PMC_COMMIT[0]),
                          "algorithmic_bytes_per_launch": solve_bytes, "avg_launch_ms": solve_ms,
                          "limiter": {"what": "VALU issue at one wave per SIMD (B=65536 = 1024 waves); not HBM",
-                                     **{k: v for k, v in head_pmc.items() if k != "hbm_bytes_per_launch"}}},
+                                     **{k: v for k, v in head_pmc.items()
+                                        if k not in ("hbm_bytes_per_launch", "measured_at")}}},
             "roofline_steady_iteration": {
                 "kernel": "k_mpc_iterate<Cartpole,UNC,LDS gains,steady> (the stop-rule path's per-iteration launch; "
                           + cost_path + ")",
                 "bound": "hbm", "achieved": it_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": it_achieved / HBM_PEAK_GBS, "traffic": it_traffic, "algorithmic_bytes_per_launch": iter_bytes,
                 "avg_launch_ms": iter_ms,
-                "pmc": {k: v for k, v in it_pmc.items() if k != "hbm_bytes_per_launch"}},
+                "pmc": {k: v for k, v in it_pmc.items() if k not in ("hbm_bytes_per_launch", "measured_at")},
+                "pmc_measured_at": it_pmc.get("measured_at")},
             "roofline_dense_cost": dense,
             "riccati_roofline": {"kernel": "k_lqr_backward<5,1,UNC> (standalone sweep, F from HBM)",
                                  "bound": "hbm", "achieved": sweep_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

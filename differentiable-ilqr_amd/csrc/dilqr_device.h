@@ -487,12 +487,12 @@ struct DenseF {
 
 template <int D>
 DEV bool bitwise_symmetric(const float (&C)[D][D]) {
-  bool sym = true;
+  unsigned asym = 0u;                       // an xor/or reduction, one compare
 #pragma unroll
   for (int i = 0; i < D; ++i)
 #pragma unroll
-    for (int j = i + 1; j < D; ++j) sym &= __float_as_uint(C[i][j]) == __float_as_uint(C[j][i]);
-  return sym;
+    for (int j = i + 1; j < D; ++j) asym |= __float_as_uint(C[i][j]) ^ __float_as_uint(C[j][i]);
+  return asym == 0u;
 }
 
 template <int N, int M>

@@ -133,6 +133,8 @@ constexpr bool packed_diag_ok() { return (2 * d) % 4 == 0; }
 // diag(q), p over the horizon: il_env.py:159-162, mpc_explicit.py:203-224)
 constexpr unsigned char kCostSym = 1, kCostDiag = 2, kCostTinv = 4;
 
+// (bitwise tests as xor/or reductions with one compare each, not a compare
+// and a mask update per entry)
 template <int d>
 DEV void pack_cost(const float (&C)[d][d], const float (&c)[d], float (&buf)[packed_cost_floats<d>()], bool& sym,
                    bool& diag) {
@@ -141,14 +143,26 @@ DEV void pack_cost(const float (&C)[d][d], const float (&c)[d], float (&buf)[pac
   for (int i = 0; i < d; ++i) buf[k++] = C[i][i];
 #pragma unroll
   for (int i = 0; i < d; ++i) buf[k++] = c[i];
+  unsigned asym = 0u, offd = 0u;
 #pragma unroll
   for (int i = 0; i < d; ++i)
 #pragma unroll
     for (int j = i + 1; j < d; ++j) {
-      sym &= __float_as_uint(C[i][j]) == __float_as_uint(C[j][i]);
-      diag &= __float_as_uint(C[i][j]) == 0u && __float_as_uint(C[j][i]) == 0u;
+      asym |= __float_as_uint(C[i][j]) ^ __float_as_uint(C[j][i]);
+      offd |= __float_as_uint(C[i][j]) | __float_as_uint(C[j][i]);
       buf[k++] = C[i][j];
     }
+  sym &= asym == 0u;
+  diag &= offd == 0u;
+}
+
+// every word of a and b equal, bit for bit
+template <int K>
+DEV bool same_bits(const float (&a)[K], const float (&b)[K]) {
+  unsigned dif = 0u;
+#pragma unroll
+  for (int k = 0; k < K; ++k) dif |= __float_as_uint(a[k]) ^ __float_as_uint(b[k]);
+  return dif == 0u;
 }
 
 // TINV: a time-invariant cost (flag kCostTinv) whose copy holds ONE record,
@@ -535,9 +549,7 @@ DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restric
 #pragma unroll
           for (int k = 0; k < PK; ++k) pk_last[k] = buf[k];
         } else {
-          bool same = true;
-#pragma unroll
-          for (int k = 0; k < PK; ++k) same &= __float_as_uint(buf[k]) == __float_as_uint(pk_last[k]);
+          const bool same = same_bits(buf, pk_last);
           if (tinv && !same)                            // records t+1 .. T-2 were skipped: all equal step T-1's
             for (int s = t + 1; s < T - 1; ++s) SoaRec<PK>::store(pack_out, pk_last, T, s, B, b);
           tinv &= same;
@@ -696,13 +708,16 @@ DEV void free_slots(int cur, int best, int& sa, int& sb) {
 // picked when 4 workgroups per CU still fit the 160 KB), instead of a workspace
 // round trip through HBM/MALL every iteration.
 // FIRST: iteration 0 of the solve (reads the caller's C, c and builds the
-// packed copy; its cost flags come back in *flags_out).
+// packed copy; its cost flags come back in *flags_out).  Otherwise the cost is
+// read as the flags pk say; PREV: the current trajectory's cost is prev_cost
+// (iterations >= 1) — else the sweep sums it (iteration 0 of a whole-solve
+// launch, whose begin already built the packed copy).
 struct LaneIter {
   float cost, alpha;
   int slot;                                                 // the accepted candidate's slot
 };
 
-template <class Model, int BM, bool LG, bool FIRST>
+template <class Model, int BM, bool LG, bool FIRST, bool PREV = true>
 DEV LaneIter mpc_iteration_lane(int T, int B, int b, const Model md, const float* __restrict__ x_init,
                                 const float* __restrict__ C, const float* __restrict__ c, const Bounds& bd,
                                 float decay, int max_ls, const MpcState& S, float* __restrict__ du_sq,
@@ -735,7 +750,7 @@ DEV LaneIter mpc_iteration_lane(int T, int B, int b, const Model md, const float
       if constexpr (packed_diag_ok<n + m>()) {
         CostDiagConst<n + m> cc;
         cc.init(S.Cpk, T, B, b);
-        win = ilqr_problem<Model, BM, TRAJ_REC, true, CostDiagConst<n + m>, true>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd,
+        win = ilqr_problem<Model, BM, TRAJ_REC, true, CostDiagConst<n + m>, PREV>(T, B, b, md, x_init, cc, nullptr, nullptr, xcur, nullptr, bd,
                                                       decay, max_ls, gr, xsa, nullptr, xsb, nullptr, du_sq, cost,
                                                       alpha, b_lds, prev_cost);
       } else {
@@ -748,21 +763,21 @@ DEV LaneIter mpc_iteration_lane(int T, int B, int b, const Model md, const float
 #else
     } else if (pk & kCostDiag) {           // set by iteration 0 only when packed_diag_ok
       if constexpr (packed_diag_ok<n + m>())
-        win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m, true>, true>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr,
+        win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m, true>, PREV>(T, B, b, md, x_init, CostPacked<n + m, true>{S.Cpk, T}, nullptr,
                                                       nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb,
                                                       nullptr, du_sq, cost, alpha, b_lds, prev_cost);
       else
         __builtin_unreachable();
     } else if ((pk & (kCostSym | kCostTinv)) == (kCostSym | kCostTinv))
-      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m, false, true>, true>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T},
+      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m, false, true>, PREV>(T, B, b, md, x_init, CostPacked<n + m, false, true>{S.Cpk, T},
                                                     nullptr, nullptr, xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr,
                                                     xsb, nullptr, du_sq, cost, alpha, b_lds, prev_cost);
     else if (pk & kCostSym)
-      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m>, true>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
+      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostPacked<n + m>, PREV>(T, B, b, md, x_init, CostPacked<n + m>{S.Cpk, T}, nullptr, nullptr,
                                                     xcur, nullptr, bd, decay, max_ls, gr, xsa, nullptr, xsb, nullptr,
                                                     du_sq, cost, alpha, b_lds, prev_cost);
     else
-      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostFull<n + m>, true>(T, B, b, md, x_init, full, nullptr, nullptr, xcur, nullptr, bd,
+      win = ilqr_problem<Model, BM, TRAJ_REC, true, CostFull<n + m>, PREV>(T, B, b, md, x_init, full, nullptr, nullptr, xcur, nullptr, bd,
                                                     decay, max_ls, gr, xsa, nullptr, xsb, nullptr, du_sq, cost,
                                                     alpha, b_lds, prev_cost);
 #endif
@@ -914,29 +929,100 @@ constexpr int slot_layout_nm(int n, int m) { return n + m <= 8 ? TRAJ_REC : TRAJ
 // get_traj(u_init) of problem b into slot 0 (util.py:104-127; u_init: the
 // caller's [T,B,m] controls, or null for zeros, the MPC default) and its slot
 // indices reset; the states and controls are written in one pass.
-template <class Model>
-DEV void mpc_begin_lane(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
-                        const float* __restrict__ u_init, const MpcState& S) {
-  constexpr int n = Model::N, m = Model::M;
+// the begin pass's cost prefetch distance in steps: 2, 3 and 4 measured no
+// faster than 1 (solve 0.386-0.391 ms for each, A/B on one box; the pass
+// streams C at ~5 TB/s, its loads and its slot-record stores interleaved)
+#ifndef DILQR_BEGIN_PF
+#define DILQR_BEGIN_PF 1
+#endif
+// ANALYSE (the whole-solve launch with a packed cost copy): the same pass also
+// streams the caller's C_t, c_t (one step ahead in registers), builds the
+// solve's packed copy and returns the problem's cost flags, exactly as
+// iteration 0's sweep does otherwise (ilqr_problem pack_out: same records,
+// the same single t = T-1 record for a time-invariant cost, same flags) — so
+// the C stream overlaps the light rollout instead of the Riccati sweep, and
+// iteration 0 runs on the packed copy like every later iteration.
+template <class Model, bool ANALYSE = false>
+DEV unsigned mpc_begin_lane(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
+                            const float* __restrict__ u_init, const MpcState& S,
+                            const float* __restrict__ C = nullptr, const float* __restrict__ c = nullptr) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  constexpr int PK = packed_cost_floats<d>();
   S.slot[b] = 0; S.slot[B + b] = 0;
   constexpr int TL = slot_layout<Model>();
-  float xt[n];
-  ld(xt, x_init + (size_t)b * n);
-  for (int t = 0; t < T; ++t) {
-    float ut[m], xn[n];
+  const CostFull<d> full{C, c};
+  // the inputs of steps t+1 .. t+PFB (cost and control) are in flight while
+  // step t runs; the loop is unrolled by PFB so the buffers rotate by name, not
+  // by copies.  The control is loaded with the cost, not after it: vmcnt counts
+  // in issue order, so a control load issued behind the cost prefetch would
+  // make its wait drain the prefetch too.
+  constexpr int PFB = ANALYSE ? DILQR_BEGIN_PF : 1;
+  float Cq[PFB][d][d], cq[PFB][d], uq[PFB][m];
+  auto load_step = [&](int s, int t) {
     if (u_init) {
-      ld(ut, u_init + ((size_t)t * B + b) * m);
+      ld(uq[s], u_init + ((size_t)t * B + b) * m);
     } else {
 #pragma unroll
-      for (int a = 0; a < m; ++a) ut[a] = 0.f;
+      for (int a = 0; a < m; ++a) uq[s][a] = 0.f;
     }
-    st_xu<TL>(S.Xs, S.Us, xt, ut, t, B, b);
-    if (t < T - 1) {
-      md.forward(xt, ut, xn);
+    if constexpr (ANALYSE) full.load(Cq[s], cq[s], t, B, b);
+  };
 #pragma unroll
-      for (int i = 0; i < n; ++i) xt[i] = xn[i];
+  for (int s = 0; s < PFB; ++s) load_step(s, s < T ? s : T - 1);
+  bool sym = true, diag = true, tinv = true;
+  float pk_first[PK];                                       // step 0's packed record (tinv test)
+  float xt[n];
+  ld(xt, x_init + (size_t)b * n);
+  for (int t0 = 0; t0 < T; t0 += PFB) {
+#pragma unroll
+    for (int s = 0; s < PFB; ++s) {
+      const int t = t0 + s;
+      if (t >= T) break;
+      float ut[m], xn[n];
+      float Cc[d][d], cc[d];
+#pragma unroll
+      for (int a = 0; a < m; ++a) ut[a] = uq[s][a];
+      if constexpr (ANALYSE) {
+#pragma unroll
+        for (int i = 0; i < d; ++i) {
+          cc[i] = cq[s][i];
+#pragma unroll
+          for (int j = 0; j < d; ++j) Cc[i][j] = Cq[s][i][j];
+        }
+      }
+      const int tp = t + PFB < T ? t + PFB : T - 1;
+      load_step(s, tp);
+      st_xu<TL>(S.Xs, S.Us, xt, ut, t, B, b);
+      if (t < T - 1) {
+        md.forward(xt, ut, xn);
+#pragma unroll
+        for (int i = 0; i < n; ++i) xt[i] = xn[i];
+      }
+      if constexpr (ANALYSE) {
+        float buf[PK];
+        pack_cost(Cc, cc, buf, sym, diag);
+        if (t == 0) {
+#pragma unroll
+          for (int k = 0; k < PK; ++k) pk_first[k] = buf[k];
+        } else {
+          const bool same = same_bits(buf, pk_first);
+          if (tinv && !same)                                // records 0 .. t-1 were skipped: all equal step 0's
+            for (int s_ = 0; s_ < t; ++s_) SoaRec<PK>::store(S.Cpk, pk_first, T, s_, B, b);
+          tinv &= same;
+          if (!tinv) SoaRec<PK>::store(S.Cpk, buf, T, t, B, b);
+        }
+      }
     }
   }
+  if constexpr (ANALYSE) {
+    if (tinv) SoaRec<PK>::store(S.Cpk, pk_first, T, T - 1, B, b);   // the one record a time-invariant copy keeps
+    const unsigned char f = sym ? (unsigned char)(kCostSym | (diag && packed_diag_ok<d>() ? kCostDiag : 0) |
+                                                  (tinv ? kCostTinv : 0))
+                                : 0;
+    S.cost_sym[b] = f;
+    return f;
+  }
+  return 0u;
 }
 
 // The control words and the stop rule's sync counters of a new solve.
@@ -978,11 +1064,15 @@ __global__ void __launch_bounds__(kBlock) k_mpc_solve_fixed(int T, int B, const 
   if (b >= B) return;
   Model md; md.load(theta);
   extern __shared__ __attribute__((aligned(16))) float lds_gains[];
-  mpc_begin_lane<Model>(T, B, b, md, x_init, u_init, S);
+  // begin; with a packed copy it also reads C once and sets the cost flags, and
+  // iteration 0 then reads the cost as every later iteration does (its sweep
+  // sums the current trajectory's cost: nothing before it did); without one
+  // (pk = 0) iteration 0 reads the caller's C like the per-launch path
+  const unsigned pk = S.Cpk ? mpc_begin_lane<Model, true>(T, B, b, md, x_init, u_init, S, C, c)
+                            : mpc_begin_lane<Model>(T, B, b, md, x_init, u_init, S);
   DILQR_STAMP(1);
-  unsigned pk = 0;
-  LaneIter r = mpc_iteration_lane<Model, BM, LG, true>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S, S.du_sq,
-                                                       lds_gains, 0, 0, 0u, 0.f, &pk);
+  LaneIter r = mpc_iteration_lane<Model, BM, LG, false, false>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
+                                                               S.du_sq, lds_gains, 0, 0, pk, 0.f);
   int cur = r.slot, best = r.slot, best_iter = 0;
   float best_cost = r.cost;
   bool take = true;

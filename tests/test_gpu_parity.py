@@ -494,6 +494,39 @@ def test_fixed_count_solve_equals_stop_rule_path(golden, name):
     assert torch.equal(a.full_du_norm, sv.full_du_norm)
 
 
+@pytest.mark.parametrize("mname", ["cartpole", "pendulum"])
+def test_tensor_bounds_whole_solve(golden, mname):
+    """Per-(t,b) bounds ([T,B,m] tensors, mpc_explicit.py:186-201) through the
+    whole-solve launch: equal to scalar bounds when every entry equals them
+    (bit for bit), and per-(t,b) random bounds equal the unfused pipeline
+    (linearise -> Riccati+pnqp -> line search kernels) bit for bit."""
+    from dilqr import ops
+    g = golden("mpc_f64")
+    name = "cart_box10" if mname == "cartpole" else "pend_box"
+    _m, T, it, (lo, hi), _eps, _nil, decay, mls = MPC_CASES[name]
+    dx = dilqr_models()[mname]()
+    x0 = gpu(g[f"{name}_x0"])
+    B, m = x0.shape[0], dx.n_ctrl
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV).contiguous()
+    c = p.repeat(T, B, 1).to(DEV).contiguous()
+    theta = ops.theta_of(dx, x0)
+    kw = dict(lqr_iter=it, eps=0.0, linesearch_decay=decay, max_linesearch_iter=mls, not_improved_lim=10 ** 9)
+    xs, us, cs, *_ = ops.mpc_solve(dx.model_id, theta, x0, C, c, T, u_lower=lo, u_upper=hi, **kw)
+    lo_t = torch.full((T, B, m), lo, device=DEV)
+    hi_t = torch.full((T, B, m), hi, device=DEV)
+    xt, ut, ct, *_ = ops.mpc_solve(dx.model_id, theta, x0, C, c, T, u_lower=lo_t, u_upper=hi_t, **kw)
+    assert same_bits(xs, xt) and same_bits(us, ut) and same_bits(cs, ct)
+    gen = torch.Generator().manual_seed(11)
+    lo_r = (lo * (0.3 + 0.7 * torch.rand(T, B, m, generator=gen))).to(DEV)
+    hi_r = (hi * (0.3 + 0.7 * torch.rand(T, B, m, generator=gen))).to(DEV)
+    xf, uf, cf, *_ = ops.mpc_solve(dx.model_id, theta, x0, C, c, T, u_lower=lo_r, u_upper=hi_r, **kw)
+    ws = ops.mpc_solve_unfused(dx.model_id, theta, x0, C, c, T, u_lower=lo_r, u_upper=hi_r, **kw)
+    assert same_bits(xf, ws.best_x) and same_bits(uf, ws.best_u) and same_bits(cf, ws.best_cost)
+    assert bool(((uf >= lo_r) & (uf <= hi_r)).all())
+    assert not same_bits(uf, us)                       # the per-(t,b) bounds took effect
+
+
 @pytest.mark.parametrize("name,warm", [("cart_unc", False), ("cart_box10", True), ("pend_box", False),
                                        ("pend_unc", True), ("rocket_unc", False)])
 def test_whole_solve_launch_equals_per_iteration_launches(golden, name, warm):

@@ -70,21 +70,39 @@ def main(pmc_dir, round_tag):
         med["launches"] = max(len(v) for v in cs.values())
         med.update(derived(med))
         out[k] = med
-    os.makedirs(os.path.join(ROOT, "profiles", round_tag), exist_ok=True)
-    json.dump(out, open(os.path.join(ROOT, "profiles", round_tag, "pmc_summary.json"), "w"), indent=1)
     try:
         head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
                               text=True).stdout.strip()
     except OSError:
         head = "?"
+    for v in out.values():
+        v["measured_at"] = head
+    # merge: kernels of the families not profiled in this run keep their entries
+    # (each tagged with the commit it was measured at)
+    os.makedirs(os.path.join(ROOT, "profiles", round_tag), exist_ok=True)
+    summ_path = os.path.join(ROOT, "profiles", round_tag, "pmc_summary.json")
+    try:
+        old_summ = json.load(open(summ_path))
+    except (OSError, ValueError):
+        old_summ = {}
+    json.dump({**old_summ, **out}, open(summ_path, "w"), indent=1)
     keep = ("hbm_bytes_per_launch", "fetch_bytes_raw", "write_bytes_raw", "valu_busy", "waitcnt_stall", "issue_stall",
-            "lds_busy", "valu_instr_per_wave", "lds_instr_per_wave")
+            "lds_busy", "valu_instr_per_wave", "lds_instr_per_wave", "salu_instr_per_wave", "measured_at")
+    traffic_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        old_t = json.load(open(traffic_path))
+    except (OSError, ValueError):
+        old_t = {}
+    old_k = old_t.get("kernels", {})
+    for v in old_k.values():
+        v.setdefault("measured_at", old_t.get("measured_at_commit", "?"))
     t = {"note": "per kernel instantiation, median launch: HBM-side bytes per launch = (2*FETCH_SIZE + "
                  "WRITE_SIZE)*1024 (gfx950 FETCH_SIZE = half the bytes, MI355X_MICROARCH.md; "
-                 f"profiles/r02/pmc_calibration.json), issue fractions of SQ_WAVE_CYCLES; profiles/{round_tag}/"
-                 "pmc_summary.json", "measured_at_commit": head,
-         "kernels": {k: {f: v[f] for f in keep if f in v} for k, v in out.items()}}
-    json.dump(t, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+                 "profiles/r02/pmc_calibration.json), issue fractions of SQ_WAVE_CYCLES; profiles/<round>/"
+                 "pmc_summary.json; measured_at: the commit each kernel's counters were taken at",
+         "measured_at_commit": head,
+         "kernels": {**old_k, **{k: {f: v[f] for f in keep if f in v} for k, v in out.items()}}}
+    json.dump(t, open(traffic_path, "w"), indent=1)
     for k, v in t["kernels"].items():
         print(k, json.dumps({f: round(x, 4) if isinstance(x, float) and x < 100 else x for f, x in v.items()}))
 
