@@ -70,12 +70,23 @@ DEV void sincos_quadrant(int q, float s1, float c1, float& s, float& c) {
   s = (q & 2) ? -ss : ss;
   c = ((q + 1) & 2) ? -cc : cc;
 }
+// The sine and cosine chains written interleaved, step by step (the same
+// operations, so the same bits): on gfx950 a packed-math result read by the
+// next instruction costs a wait state (s_nop), and alternating the two
+// independent chains gives each result one instruction of distance.
 template <class S>
 DEV void sincos_poly(S r, S& s1, S& c1) {
   const S z = r * r;
-  s1 = vfma(vfma(vfma(S(-1.9515295891e-4f), z, S(8.3321608736e-3f)), z, S(-1.6666654611e-1f)) * z, r, r);
-  c1 = vfma(vfma(vfma(S(2.443315711809948e-5f), z, S(-1.388731625493765e-3f)), z, S(4.166664568298827e-2f)),
-            z * z, S(-0.5f) * z) + S(1.0f);
+  S a = vfma(S(-1.9515295891e-4f), z, S(8.3321608736e-3f));
+  S b = vfma(S(2.443315711809948e-5f), z, S(-1.388731625493765e-3f));
+  a = vfma(a, z, S(-1.6666654611e-1f));
+  b = vfma(b, z, S(4.166664568298827e-2f));
+  const S zz = z * z;
+  const S h = S(-0.5f) * z;
+  a = a * z;
+  b = vfma(b, zz, h);
+  s1 = vfma(a, r, r);
+  c1 = b + S(1.0f);
 }
 // The reduction-and-polynomial path runs unconditionally (branch-free);
 // lanes whose argument is out of its range are patched afterwards in a branch

@@ -1,8 +1,8 @@
 // dilqr_implicit_group.h — the DiLQR implicit backward (k_implicit_backward,
-// dilqr_kernels.hip) for the 16-lanes-per-problem models (rocket, d = 16).
-// Included by dilqr_kernels.hip after dilqr_group.h.
+// tu_implicit.hip) for the 16-lanes-per-problem models (rocket, d = 16).
+// Included by tu_implicit_rocket.hip after dilqr_group.h.
 //
-// Same four passes and the same algebra as the one-lane kernel
+// Same three passes (B down, A+C up, D down) and the same algebra as the one-lane kernel
 // (oracle/adjoint.py implicit_backward_fast; lqr_step_explicit.py:653-712 with
 // rocket's grad_input, rocket.py:263-323, and its build_batched_* tables,
 // rocket.py:541-820), distributed by rows: lane r owns row r of every d x d or
@@ -73,57 +73,6 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
 #pragma unroll
     for (int a = 0; a < m; ++a) ut[a] = u[tb * m + a];
   };
-  // ---------------- A: gradx_t, t = 0..T-1 (grad_input, rocket.py:263-323 / cartpole.py:755-769)
-  {
-    float gx[p];
-#pragma unroll
-    for (int k = 0; k < p; ++k) gx[k] = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const size_t tb = (size_t)t * B + b;
-      if (t > 0) {
-        if (r < n) {
-#pragma unroll
-          for (int k = 0; k < p; ++k) I.gx[r][k] = gx[k];
-        }
-        __syncthreads();
-        float xt[n], ut[m];
-        load_tau(tb, xt, ut);
-        float Kq[m][n];                                   // K[t-1] of the reversed stack = K_{T-t}
-        const float* Kp = K + ((size_t)(T - t) * B + b) * m * n;
-#pragma unroll
-        for (int a = 0; a < m; ++a)
-#pragma unroll
-          for (int l = 0; l < n; ++l) Kq[a][l] = Kp[a * n + l];
-        if (r < n) {
-          float xx[n], Dr[d], ft[p];
-          D2::xx_row(r, theta, xt, ut, xx);
-          md.template jac_row<false>(r, xt, ut, Dr);
-          D2::xth_row(r, theta, xt, ut, ft);
-          float A[n];
-#pragma unroll
-          for (int l = 0; l < n; ++l) {
-            float s = xx[l];
-#pragma unroll
-            for (int a = 0; a < m; ++a) s += Dr[n + a] * Kq[a][l];
-            A[l] = s;
-          }
-#pragma unroll
-          for (int k = 0; k < p; ++k) {
-            float s = 0.f;
-#pragma unroll
-            for (int l = 0; l < n; ++l) s += A[l] * I.gx[l][k];
-            gx[k] = ft[k] + s;
-          }
-        }
-        __syncthreads();
-      }
-      if (valid && r < n) {
-        float* R0 = rec(t);
-#pragma unroll
-        for (int k = 0; k < p; ++k) R0[W::GX + k * kG + r] = gx[k];
-      }
-    }
-  }
   // ---------------- B: costates, M_t, Riccati of the C + M^T problem (active set masked)
   {
     if (r < n) {
@@ -209,19 +158,35 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
       __syncthreads();
     }
   }
-  // ---------------- C: rollout y of the modified problem (linear, alpha = 1)
+  // ---------------- A + C (t up): gradx_t (grad_input, rocket.py:263-323 /
+  // cartpole.py:755-769) and the rollout y of the modified problem (linear,
+  // alpha = 1) in ONE pass: both walk t upward over the same (x_t, u_t) and share
+  // the Jacobian row and the step's two barriers — one latency-bound pass over T
+  // fewer than running them apart, the same arithmetic.
   {
+    float gx[p];
+#pragma unroll
+    for (int k = 0; k < p; ++k) gx[k] = 0.f;
     float yx = 0.f;                                        // lane r < n: y_t[r]
     for (int t = 0; t < T; ++t) {
       const size_t tb = (size_t)t * B + b;
       float* R0 = rec(t);
-      float Kc[m], kt[m], ut[m], xt[n];
+      float xt[n], ut[m], Kc[m], kt[m];
       load_tau(tb, xt, ut);
 #pragma unroll
       for (int a = 0; a < m; ++a) {
         Kc[a] = r < n ? R0[W::KG + a * kG + r] : 0.f;
         kt[a] = R0[W::KG + a * kG + n];
       }
+      float Kq[m][n];                                     // K[t-1] of the reversed stack = K_{T-t}
+      if (t > 0) {
+        const float* Kp = K + ((size_t)(T - t) * B + b) * m * n;
+#pragma unroll
+        for (int a = 0; a < m; ++a)
+#pragma unroll
+          for (int l = 0; l < n; ++l) Kq[a][l] = Kp[a * n + l];
+      }
+      // C: y_t from y_t's state part (the previous step's D y)
       float yr = r < n ? yx : 0.f;
 #pragma unroll
       for (int a = 0; a < m; ++a) {
@@ -230,18 +195,49 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         yr = (r == n + a) ? ya : yr;
       }
       if (valid && r < d) R0[W::Y + r] = yr;
-      if (t < T - 1) {
-        if (r < d) I.vec[r] = yr;
+      const bool a_step = t > 0, c_step = t < T - 1;       // uniform
+      if (a_step || c_step) {
+        if (a_step && r < n) {
+#pragma unroll
+          for (int k = 0; k < p; ++k) I.gx[r][k] = gx[k];
+        }
+        if (c_step && r < d) I.vec[r] = yr;
         __syncthreads();
         if (r < n) {
           float Dr[d];
           md.template jac_row<false>(r, xt, ut, Dr);
-          float s = 0.f;
+          if (a_step) {
+            float xx[n], ft[p];
+            D2::xx_row(r, theta, xt, ut, xx);
+            D2::xth_row(r, theta, xt, ut, ft);
+            float A[n];
 #pragma unroll
-          for (int j = 0; j < d; ++j) s += Dr[j] * I.vec[j];
-          yx = s;
+            for (int l = 0; l < n; ++l) {
+              float s = xx[l];
+#pragma unroll
+              for (int a = 0; a < m; ++a) s += Dr[n + a] * Kq[a][l];
+              A[l] = s;
+            }
+#pragma unroll
+            for (int k = 0; k < p; ++k) {
+              float s = 0.f;
+#pragma unroll
+              for (int l = 0; l < n; ++l) s += A[l] * I.gx[l][k];
+              gx[k] = ft[k] + s;
+            }
+          }
+          if (c_step) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < d; ++j) s += Dr[j] * I.vec[j];
+            yx = s;
+          }
         }
         __syncthreads();
+      }
+      if (valid && r < n) {
+#pragma unroll
+        for (int k = 0; k < p; ++k) R0[W::GX + k * kG + r] = gx[k];
       }
     }
   }

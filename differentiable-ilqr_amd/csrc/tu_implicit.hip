@@ -12,13 +12,13 @@ namespace dilqr {
 // extra LQR solve with cost C_t + M_t^T, M_t = sum_i lam_{t+1,i} d D_t[i] / d tau
 // (the Lagrangian Hessian of the dynamics), after which dC, dc, dtheta are the
 // KKT gradients of the adjoint solve with r = w, whose trajectory is that same
-// solve's y.  Per problem (one lane), four passes over T:
-//   A (t up)   : gradx_t (grad_input's closed-loop d x_t / d theta, with the
-//                reference's reversed-K and x_grad_xtm1 quirks) -> ws
-//   B (t down) : primal costates lam_t -> ws; M_t; Riccati step with C_t + M_t^T,
-//                c_back = -g_t, active set masked (u_zero_I engine) -> ws
-//   C (t up)   : rollout y (no line search) -> ws
-//   D (t down) : w_t = g_t - M_t^T y_t, dlam; dC_t, dc_t out; dtheta accumulated.
+// solve's y.  Per problem (one lane), three passes over T:
+//   B (t down)   : primal costates lam_t -> ws; M_t; Riccati step with C_t + M_t^T,
+//                  c_back = -g_t, active set masked (u_zero_I engine) -> ws
+//   A+C (t up)   : gradx_t (grad_input's closed-loop d x_t / d theta, with the
+//                  reference's reversed-K and x_grad_xtm1 quirks) and the rollout
+//                  y (no line search) -> ws, one Jacobian per step for both
+//   D (t down)   : w_t = g_t - M_t^T y_t, dlam; dC_t, dc_t out; dtheta accumulated.
 template <class Model> struct ImplicitWs {
   static constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m;
   static constexpr int GX = 0, LAM = n * p, KG = LAM + n, Y = KG + m * n + m;
@@ -42,49 +42,6 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     if (bd.mode == DILQR_BOUNDS_NONE) return false;
     return fabsf(ua - bound_lo(bd, tb * m + a)) <= 1e-8f || fabsf(ua - bound_hi(bd, tb * m + a)) <= 1e-8f;
   };
-  // ---------------- A: gradx_t, t = 0..T-1  (cartpole.py:755-769)
-  {
-    float gx[n][p];
-#pragma unroll
-    for (int i = 0; i < n; ++i)
-#pragma unroll
-      for (int k = 0; k < p; ++k) gx[i][k] = 0.f;
-    st2(rec(0) + W::GX, gx);
-    for (int t = 1; t < T; ++t) {
-      size_t tb = (size_t)t * B + b;
-      float xt[n], ut[m], D[n][d], ft[n][p], Kq[m][n];
-      ld(xt, x + tb * n); ld(ut, u + tb * m);
-      md.jacobian(xt, ut, D);
-      D2::f_theta(theta, xt, ut, ft);
-      ld2(Kq, K + ((size_t)(T - t) * B + b) * m * n);     // K[t-1] of the reversed stack = K_{T-t}
-      float A[n][n];
-#pragma unroll
-      for (int i = 0; i < n; ++i)
-#pragma unroll
-        for (int l = 0; l < n; ++l) {
-          float s = D[i][l];
-          if (D2Of<Model>::XX00_ZERO && i == 0 && l == 0) s = 0.f;
-#pragma unroll
-          for (int a = 0; a < m; ++a) s += D[i][n + a] * Kq[a][l];
-          A[i][l] = s;
-        }
-      float ng[n][p];
-#pragma unroll
-      for (int i = 0; i < n; ++i)
-#pragma unroll
-        for (int k = 0; k < p; ++k) {
-          float s = 0.f;
-#pragma unroll
-          for (int l = 0; l < n; ++l) s += A[i][l] * gx[l][k];
-          ng[i][k] = ft[i][k] + s;
-        }
-#pragma unroll
-      for (int i = 0; i < n; ++i)
-#pragma unroll
-        for (int k = 0; k < p; ++k) gx[i][k] = ng[i][k];
-      st2(rec(t) + W::GX, gx);
-    }
-  }
   // ---------------- B: costates, M_t, Riccati of the C + M^T problem
   {
     RiccatiState<n, m> rs;
@@ -149,41 +106,81 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       for (int i = 0; i < n; ++i) { lam[i] = nl[i]; r[W::LAM + i] = nl[i]; }
     }
   }
-  // ---------------- C: rollout y of the modified problem (linear, alpha = 1)
+  // ---------------- A + C (t up): gradx_t (grad_input's closed-loop d x_t /
+  // d theta, cartpole.py:755-769) and the rollout y of the modified problem
+  // (linear, alpha = 1) in ONE pass: both walk t upward over the same (x_t, u_t)
+  // and share the Jacobian D_t — one latency-bound pass over T fewer than
+  // running them apart, the same arithmetic.
   {
-    float yx[n];
+    float gx[n][p], yx[n];
 #pragma unroll
-    for (int i = 0; i < n; ++i) yx[i] = 0.f;
+    for (int i = 0; i < n; ++i) {
+      yx[i] = 0.f;
+#pragma unroll
+      for (int k = 0; k < p; ++k) gx[i][k] = 0.f;
+    }
+    st2(rec(0) + W::GX, gx);
     for (int t = 0; t < T; ++t) {
       size_t tb = (size_t)t * B + b;
       float* r = rec(t);
-      float Kt[m][n], kt[m], ut[m];
+      float xt[n], ut[m], Kt[m][n], kt[m];
+      ld(xt, x + tb * n); ld(ut, u + tb * m);
       ld2(Kt, r + W::KG);
 #pragma unroll
       for (int a = 0; a < m; ++a) kt[a] = r[W::KG + m * n + a];
-      ld(ut, u + tb * m);
+      float Kq[m][n];
+      if (t >= 1) ld2(Kq, K + ((size_t)(T - t) * B + b) * m * n);   // K[t-1] of the reversed stack = K_{T-t}
+      float D[n][d];
+      md.jacobian(xt, ut, D);
+      if (t >= 1) {
+        float ft[n][p];
+        D2::f_theta(theta, xt, ut, ft);
+        float A[n][n];
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int l = 0; l < n; ++l) {
+            float s_ = D[i][l];
+            if (D2Of<Model>::XX00_ZERO && i == 0 && l == 0) s_ = 0.f;
+#pragma unroll
+            for (int a = 0; a < m; ++a) s_ += D[i][n + a] * Kq[a][l];
+            A[i][l] = s_;
+          }
+        float ng[n][p];
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int k = 0; k < p; ++k) {
+            float s_ = 0.f;
+#pragma unroll
+            for (int l = 0; l < n; ++l) s_ += A[i][l] * gx[l][k];
+            ng[i][k] = ft[i][k] + s_;
+          }
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int k = 0; k < p; ++k) gx[i][k] = ng[i][k];
+        st2(r + W::GX, gx);
+      }
       float y[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) y[i] = yx[i];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
-        float s = 0.f;
+        float s_ = 0.f;
 #pragma unroll
-        for (int j = 0; j < n; ++j) s += Kt[a][j] * yx[j];
-        y[n + a] = active(tb, a, ut[a]) ? 0.f : (s + 0.f) + kt[a];
+        for (int j = 0; j < n; ++j) s_ += Kt[a][j] * yx[j];
+        y[n + a] = active(tb, a, ut[a]) ? 0.f : (s_ + 0.f) + kt[a];
       }
 #pragma unroll
       for (int i = 0; i < d; ++i) r[W::Y + i] = y[i];
       if (t < T - 1) {
-        float xt[n], D[n][d];
-        ld(xt, x + tb * n);
-        md.jacobian(xt, ut, D);
 #pragma unroll
         for (int i = 0; i < n; ++i) {
-          float s = 0.f;
+          float s_ = 0.f;
 #pragma unroll
-          for (int j = 0; j < d; ++j) s += D[i][j] * y[j];
-          yx[i] = s;
+          for (int j = 0; j < d; ++j) s_ += D[i][j] * y[j];
+          yx[i] = s_;
         }
       }
     }

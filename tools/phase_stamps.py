@@ -69,6 +69,18 @@ if SOLVE:
     out["kernel_span_us"] = float(np.median([(x[:, 7].max() - x[:, 6].min()) / 100.0 for x in rows[1:]]))
     out["wave_end_spread_us"] = float(np.median([(x[:, 7].max() - x[:, 7].min()) / 100.0 for x in rows[1:]]))
     out["wave_start_spread_us"] = float(np.median([(x[:, 6].max() - x[:, 6].min()) / 100.0 for x in rows[1:]]))
+    # by XCD (workgroups go round-robin over the 8 XCDs: wave w on XCD w % 8):
+    # wall time of each wave (100 MHz ticks) and its shader clock
+    wall = np.stack([(x[:, 7] - x[:, 6]) / 100.0 for x in rows[1:]])           # [solves, W] us
+    clk = np.stack([(x[:, 5] - x[:, 0]) / ((x[:, 7] - x[:, 6]) / 100e6) / 1e9 for x in rows[1:]])
+    out["by_xcd"] = {str(k): {"wave_us_median": float(np.median(wall[:, k::8])),
+                              "wave_us_max": float(wall[:, k::8].max()),
+                              "clock_ghz_median": float(np.median(clk[:, k::8]))} for k in range(8)}
+    # is a slow wave slow in every solve (place) or in one (data)?
+    per_wave = wall.mean(0)
+    out["wave_us_p50_p90_max_of_solve_means"] = [float(np.median(per_wave)), float(np.percentile(per_wave, 90)),
+                                                 float(per_wave.max())]
+    out["slowest_wave_rank_corr"] = float(np.corrcoef(wall[0], wall[-1])[0, 1])
     print(json.dumps(out))
     sys.exit(0)
 for solve in range(4):
