@@ -396,6 +396,9 @@ def secondary_configs(dev):
         bd, keep = N.make_bounds(-lim, lim)
         val, ms_it = _timed_solves(sv, N.MODEL_CARTPOLE, theta, x0, C, c, bd, 0.5, 2, 10, 3, 1)
         active = float(((sv.gather_best()[1].abs() - lim).abs() < 1e-6).float().mean())
+        # the timed solves' launch (k_mpc_solve_fixed<Cartpole,BOX> + finish), event-timed
+        s_ms = _event_ms(stream, lambda r: sv.solve_fixed(N.MODEL_CARTPOLE, theta, x0, C, c, bd, 0.5, 2, 1e-4), 5)
+        sb = float(solve_bytes_per_problem(sv.cost_sym.cpu().numpy(), 10).sum())
         sv2 = ops.MPCSolve(T, B, n, m, dev)
         k_ms = steady_iteration_ms(sv2, N.MODEL_CARTPOLE, theta, x0, C, c, bd, 0.5, 2, dev)
         kb = float(iter_bytes_per_problem(iter_cost_floats(sv2.cost_sym.cpu().numpy())).sum())
@@ -403,9 +406,15 @@ def secondary_configs(dev):
         out[f"config4_cartpole_box{int(lim)}"] = {
             "value": val, "unit": "problem-iters/s", "ms_per_iter": ms_it, "batch": B, "T": T,
             "active_control_frac": active,
-            "fused_iteration": with_pmc(
-                {"kernel": "k_mpc_iterate<Cartpole,BOX,LDS gains,steady>", "bound": "hbm",
-                 "avg_launch_ms": k_ms, "algorithmic_bytes_per_launch": kb,
+            "solve_launch": with_pmc(
+                {"kernel": "k_mpc_solve_fixed<Cartpole,BOX,LDS gains> + k_mpc_fixed_finish (the timed solves)",
+                 "bound": "hbm", "avg_launch_ms": s_ms, "algorithmic_bytes_per_launch": sb,
+                 "achieved": sb / (s_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": sb / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                "k_mpc_solve_fixed<Cartpole, 1, true>" if lim == 100.0 else "-"),
+            "steady_iteration": with_pmc(
+                {"kernel": "k_mpc_iterate<Cartpole,BOX,LDS gains,steady> (the stop-rule path's per-iteration launch)",
+                 "bound": "hbm", "avg_launch_ms": k_ms, "algorithmic_bytes_per_launch": kb,
                  "achieved": kb / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": kb / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
                 "k_mpc_iterate<Cartpole, 1, true, false>" if lim == 100.0 else "-")}
@@ -478,6 +487,9 @@ def profile_set(name, dev):
         bd, _ = N.make_bounds(-100.0, 100.0)
         out["box_iter_ms"] = steady_iteration_ms(ops.MPCSolve(T, B, 5, 1, dev), N.MODEL_CARTPOLE, theta, x0, C, c,
                                                  bd, 0.5, 2, dev, reps=4)
+        sv = ops.MPCSolve(T, B, 5, 1, dev, fixed_iters=10)             # the timed solves' launch
+        out["box_solve_ms"] = _event_ms(torch.cuda.current_stream(dev), lambda r: sv.solve_fixed(
+            N.MODEL_CARTPOLE, theta, x0, C, c, bd, 0.5, 2, 1e-4), 3)
     elif name == "implicit":                      # both implicit backward kernels (config 4 and 3 shapes)
         from dilqr.env_dx.cartpole import CartpoleDx
         for model, T, B, lim in (("cartpole", 25, 65536, 10.0), ("rocket", 30, 32768, None)):
