@@ -1099,6 +1099,23 @@ __global__ void __launch_bounds__(kBlock) k_mpc_solve_fixed(int T, int B, const 
 }
 
 // ---------------------------------------------------------------- launchers
+// Gain records in LDS (lds bytes per 64-problem workgroup) when four
+// workgroups per CU fit — one wave per SIMD at the headline's 65536 problems —
+// or when the whole grid fits the chip's LDS in one round anyway (a small
+// batch with a long horizon: the IL loop's T = 35, 4096 problems), and a
+// workgroup's share stays within the 64 KiB a launch may take without opting in.
+inline bool lds_gains_fit(size_t lds, int B) {
+  if (kNoLdsGains || lds > 65536) return false;
+  if (lds * 4 <= kLdsPerCU) return true;
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return n;
+  }();
+  return (size_t)grid_for(B) <= (size_t)cus * (kLdsPerCU / lds);
+}
 // the fused MPC iteration of one thread-per-problem model: bounds mode, gain
 // records in LDS when four workgroups per CU still fit, iteration 0's own
 // instantiation
@@ -1111,7 +1128,7 @@ int launch_mpc_step_tpp(const MpcStepArgs& a) {
 #define LAUNCH_MPC(BM_)                                                                                      \
   do {                                                                                                       \
     const size_t lds = (size_t)a.T * kBlock * (MD::N * MD::M + MD::M) * sizeof(float);                      \
-    const bool lg = lds * 4 <= kLdsPerCU && !kNoLdsGains;                                                   \
+    const bool lg = lds_gains_fit(lds, a.B);                                                                 \
     if (a.iteration == 0 && lg) LAUNCH_IT(BM_, true, true, lds);                                             \
     else if (a.iteration == 0) LAUNCH_IT(BM_, false, true, 0);                                               \
     else if (lg) LAUNCH_IT(BM_, true, false, lds);                                                           \
@@ -1131,7 +1148,7 @@ int launch_mpc_solve_tpp(const MpcSolveArgs& a) {
 #define LAUNCH_SOLVE(BM_)                                                                                    \
   do {                                                                                                       \
     const size_t lds = (size_t)a.T * kBlock * (MD::N * MD::M + MD::M) * sizeof(float);                      \
-    if (lds * 4 <= kLdsPerCU && !kNoLdsGains)                                                                \
+    if (lds_gains_fit(lds, a.B))                                                                             \
       k_mpc_solve_fixed<MD, BM_, true><<<grid_for(a.B), kBlock, lds, a.stream>>>(                             \
           a.T, a.B, a.theta, a.x_init, a.u_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iters, a.best_cost_eps, a.st); \
     else                                                                                                     \

@@ -379,6 +379,19 @@ int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const flo
   return dilqr_mpc_stop_rule_f32(T, m, B, iteration, st, stream);
 }
 
+int dilqr_mpc_iterate_range_f32(int model, int T, int B, const float* theta, const float* x_init, const float* C,
+                                const float* c, dilqr_bounds bounds, float linesearch_decay, int max_linesearch_iter,
+                                int first_iteration, int count, float best_cost_eps, float eps, int not_improved_lim,
+                                dilqr_mpc_state st, void* stream) {
+  if (count < 0 || first_iteration < 0) return DILQR_E_ARG;
+  for (int i = first_iteration; i < first_iteration + count; ++i) {
+    const int e = dilqr_mpc_iterate_f32(model, T, B, theta, x_init, C, c, bounds, linesearch_decay,
+                                        max_linesearch_iter, i, best_cost_eps, eps, not_improved_lim, st, stream);
+    if (e) return e;
+  }
+  return 0;
+}
+
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out, float* u_out,
                               void* stream) {
   if (T < 1 || B < 0 || !x_out || !u_out || !al16(x_out) || !al16(u_out) || bad_state(st)) return DILQR_E_ARG;

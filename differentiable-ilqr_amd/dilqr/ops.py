@@ -277,6 +277,16 @@ class MPCSolve:
                int(min(not_improved_lim, 2 ** 31 - 1)), self.state, N.stream(x_init.device))
         self.last_iteration = int(iteration)
 
+    def iterate_range(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, first, count, best_cost_eps, eps,
+                      not_improved_lim):
+        """Iterations first .. first+count-1 in one library call (the same
+        launches as iterate() for each)."""
+        N.call("dilqr_mpc_iterate_range_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init), N.ptr(C),
+               N.ptr(c), bounds, float(decay), int(max_ls), int(first), int(count), float(best_cost_eps), float(eps),
+               int(min(not_improved_lim, 2 ** 31 - 1)), self.state, N.stream(x_init.device))
+        if count > 0:
+            self.last_iteration = int(first + count - 1)
+
     def iterate_fixed(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, iteration, best_cost_eps):
         """Iteration `iteration` of a fixed-count solve (one launch, no stop rule)."""
         if not self.fixed_iters or not 0 <= iteration < self.fixed_iters:
@@ -339,10 +349,13 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
         x, u = sv.gather_best()
         return x, u, sv.best_cost, sv.best_du, sv
     sv.begin(model_id, theta, x_init, u_init)
-    for i in range(lqr_iter):
-        sv.iterate(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i,
-                   best_cost_eps, eps, not_improved_lim)
-        if check_every and (i + 1) % check_every == 0 and i + 1 < lqr_iter and sv.stopped:
+    # runs of check_every iterations per library call, the stop flag polled
+    # between runs (iterations after a stop are device no-ops)
+    step = check_every if check_every else lqr_iter
+    for i0 in range(0, lqr_iter, step):
+        sv.iterate_range(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i0,
+                         min(step, lqr_iter - i0), best_cost_eps, eps, not_improved_lim)
+        if i0 + step < lqr_iter and sv.stopped:
             break
     del keep
     x, u = sv.gather_best()

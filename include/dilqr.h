@@ -61,7 +61,7 @@ typedef struct dilqr_bounds {
   const float* hi_t;             /* [T,B,m] or NULL                              */
 } dilqr_bounds;
 
-/* Library version (for the loader's sanity check): 6. */
+/* Library version (for the loader's sanity check): 7. */
 int dilqr_version(void);
 
 /* Build id: the first 16 hex digits of the sha256 of the sources the library
@@ -315,6 +315,16 @@ int dilqr_mpc_iterate_f32(int model, int T, int B, const float* theta, const flo
                           float linesearch_decay, int max_linesearch_iter, int iteration,
                           float best_cost_eps, float eps, int not_improved_lim,
                           dilqr_mpc_state st, void* stream);
+/* Iterations first_iteration .. first_iteration+count-1 of the same solve in
+   one call (ABI 7): dilqr_mpc_iterate_f32 for each, in order — the host
+   launches a run of iterations between two polls of the stop flag without a
+   foreign-function round trip per iteration (iterations after a stop are
+   device no-ops either way). */
+int dilqr_mpc_iterate_range_f32(int model, int T, int B, const float* theta, const float* x_init,
+                                const float* C, const float* c, dilqr_bounds bounds,
+                                float linesearch_decay, int max_linesearch_iter,
+                                int first_iteration, int count, float best_cost_eps, float eps,
+                                int not_improved_lim, dilqr_mpc_state st, void* stream);
 /* its two launches, separately (profiling) */
 int dilqr_mpc_step_f32(int model, int T, int B, const float* theta, const float* x_init,
                        const float* C, const float* c, dilqr_bounds bounds,

@@ -527,6 +527,45 @@ def test_tensor_bounds_whole_solve(golden, mname):
     assert not same_bits(uf, us)                       # the per-(t,b) bounds took effect
 
 
+@pytest.mark.parametrize("T,B,bounds", [(48, 100, None), (40, 77, (-10.0, 10.0)), (3, 130, None)])
+def test_whole_solve_hbm_gains_and_ragged_batch(T, B, bounds):
+    """The whole-solve launch off the headline shape: T = 48 puts the gain
+    records in HBM (74 KB per workgroup: over the 64 KiB a launch takes
+    without opting in), T = 40 keeps them in LDS only because the small grid
+    fits the chip in one round (61 KB per workgroup, more than four per CU
+    allow), B not a multiple of 64 leaves idle lanes in the last wave, T = 3 is
+    nearly all peeled steps — each bit-identical to the per-iteration launches,
+    with and without bounds."""
+    from dilqr import _native as N
+    from dilqr import ops
+    from dilqr.env_dx.cartpole import CartpoleDx
+    dx = CartpoleDx()
+    rng = np.random.RandomState(T * 1000 + B)
+    th = rng.uniform(-np.pi, np.pi, B)
+    x0 = gpu(np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                       rng.uniform(-1, 1, B)], 1))
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV).contiguous()
+    c = p.repeat(T, B, 1).to(DEV).contiguous()
+    theta = ops.theta_of(dx, x0)
+    lo, hi = bounds if bounds else (None, None)
+    bd, _keep = N.make_bounds(lo, hi)
+    it = 6
+    a = ops.MPCSolve(T, B, 5, 1, x0.device, fixed_iters=it)
+    a.begin(dx.model_id, theta, x0)
+    for i in range(it):
+        a.iterate_fixed(dx.model_id, theta, x0, C, c, bd, 0.5, 2, i, 1e-4)
+    a.finish_fixed(it)
+    b = ops.MPCSolve(T, B, 5, 1, x0.device, fixed_iters=it)
+    b.solve_fixed(dx.model_id, theta, x0, C, c, bd, 0.5, 2, 1e-4)
+    for key in ("slot", "cost", "alpha", "improved", "best_cost", "best_du", "full_du_norm", "best_iter"):
+        assert same_bits(getattr(a, key).float(), getattr(b, key).float()), key
+    xa, ua = a.gather_best()
+    xb, ub = b.gather_best()
+    assert torch.equal(xa, xb) and torch.equal(ua, ub)
+    assert torch.isfinite(b.best_cost).all()
+
+
 @pytest.mark.parametrize("name,warm", [("cart_unc", False), ("cart_box10", True), ("pend_box", False),
                                        ("pend_unc", True), ("rocket_unc", False)])
 def test_whole_solve_launch_equals_per_iteration_launches(golden, name, warm):
