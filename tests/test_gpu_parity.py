@@ -692,6 +692,17 @@ def test_implicit_backward_full_size():
                                        c[:, sl].contiguous(), None, None, x[:, sl].contiguous(),
                                        u[:, sl].contiguous(), K[:, sl].contiguous(), -10.0, 10.0, None)
     assert torch.equal(dth[sl], dth2) and torch.equal(dC[:, sl], dC2)
+    # the same slice with every off-diagonal entry of C written as -0.0: not
+    # bitwise a diagonal cost, so the backward re-reads C_t in its last pass
+    # instead of taking the diagonal from registers — the same values, so the
+    # same results bit for bit
+    Cz = C[:, sl].clone()
+    off = ~torch.eye(6, dtype=torch.bool, device=DEV)
+    Cz[:, :, off] = -0.0
+    dC3, dc3, dth3 = implicit_backward(dx, wx[:, sl].contiguous(), wu[:, sl].contiguous(), Cz.contiguous(),
+                                       c[:, sl].contiguous(), None, None, x[:, sl].contiguous(),
+                                       u[:, sl].contiguous(), K[:, sl].contiguous(), -10.0, 10.0, None)
+    assert torch.equal(dth3, dth2) and torch.equal(dC3, dC2) and torch.equal(dc3, dc2)
 
 
 def rocket_x0(B, seed=0):

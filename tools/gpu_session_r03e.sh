@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# implicit-backward A/B (ab/ variants) + the implicit parity tests on the in-tree build
+# implicit parity tests on the in-tree build + implicit A/B of ab/ variants
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
