@@ -93,8 +93,14 @@ class HipDynamics(nn.Module):
         d, p = n + m, N.lib().dilqr_model_num_params(self.model_id)
         dev = X.device
         Xc, Uc = X.detach().float().contiguous(), U.detach().float().contiguous()
+        Kc = None
+        if K is not None:
+            if isinstance(K, (list, tuple)):        # the reference's per-step list (lqr_backward's Ks)
+                K = torch.stack([torch.as_tensor(k) for k in K])
+            Kc = torch.as_tensor(K).detach().to(device=dev, dtype=torch.float32).contiguous()
+            if tuple(Kc.shape) != (T, B, m, n):   # k_grad_input reads K[t] for every t < T
+                raise ValueError(f"grad_input: K must be [T, B, m, n] = {(T, B, m, n)}, got {tuple(Kc.shape)}")
         D, Dp, Dx, Du, xth, xx, xu = self.get_matrices(Xc.view(T * B, n), Uc.view(T * B, m))
-        Kc = None if K is None else torch.as_tensor(K).detach().to(device=dev, dtype=torch.float32).contiguous()
         Tm = max(T - 1, 0)
         gD = torch.empty(Tm, B, n, d, p, device=dev)
         gd = torch.empty(Tm, B, n, p, device=dev)

@@ -54,6 +54,17 @@ def linearize(model_id, theta, x, u):
     return F, f
 
 
+def zero_mask(u_zero_I, T, B, m, device):
+    """u_zero_I as the kernels read it: uint8 [T,B,m] on `device` (the kernels
+    index it (t*B + b)*m + a for every t and b, so any other shape is refused
+    here rather than read out of bounds on the device)."""
+    if u_zero_I is None:
+        return None
+    if tuple(u_zero_I.shape) != (T, B, m):
+        raise ValueError(f"u_zero_I: expected [T, B, m] = {(T, B, m)}, got {tuple(u_zero_I.shape)}")
+    return u_zero_I.to(device=device, dtype=torch.uint8).contiguous()
+
+
 def lqr_backward(C, c, F, n, m, x=None, u=None, u_lower=None, u_upper=None, u_zero_I=None,
                  m_solver=N.SOLVE_INV, want_nqp=False):
     """lqr_backward (lqr_step_explicit.py:54-162) with the fused delta-space c_back.
@@ -61,7 +72,7 @@ def lqr_backward(C, c, F, n, m, x=None, u=None, u_lower=None, u_upper=None, u_ze
     T, B = C.shape[:2]
     C, c, F, x, u = _f32(C), _f32(c), _f32(F), _f32(x), _f32(u)
     bounds, keep = N.make_bounds(u_lower, u_upper)
-    zI = None if u_zero_I is None else u_zero_I.to(torch.uint8).contiguous()
+    zI = zero_mask(u_zero_I, T, B, m, C.device)
     K = torch.empty(T, B, m, n, device=C.device)
     k = torch.empty(T, B, m, device=C.device)
     nqp = torch.zeros(B, dtype=torch.int32, device=C.device) if want_nqp else None
@@ -112,7 +123,7 @@ def lqr_forward(model_id, theta, x_init, C, c, x, u, K, k, F=None, f=None, u_low
     m = u.shape[2]
     x_init, C, c, x, u, K, k, F, f = map(_f32, (x_init, C, c, x, u, K, k, F, f))
     bounds, keep = N.make_bounds(u_lower, u_upper)
-    zI = None if u_zero_I is None else u_zero_I.to(torch.uint8).contiguous()
+    zI = zero_mask(u_zero_I, T, B, m, x.device)
     dev = x.device
     nx, nu = torch.empty_like(x), torch.empty_like(u)
     cost, alpha = torch.empty(B, device=dev), torch.empty(B, device=dev)
@@ -351,7 +362,7 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     sv.begin(model_id, theta, x_init, u_init)
     # runs of check_every iterations per library call, the stop flag polled
     # between runs (iterations after a stop are device no-ops)
-    step = check_every if check_every else lqr_iter
+    step = check_every if check_every else max(lqr_iter, 1)
     for i0 in range(0, lqr_iter, step):
         sv.iterate_range(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i0,
                          min(step, lqr_iter - i0), best_cost_eps, eps, not_improved_lim)
@@ -392,7 +403,13 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
     iteration.  u_zero_I [T,B,m] (bool): controls held at zero — the sweep's
     masked solve when unconstrained (lqr_step_explicit.py:98-129; with bounds
     the reference's pnqp branch ignores the mask) and zeroed in every rollout
-    before the clamp (199-200)."""
+    before the clamp (199-200).
+
+    The host polls the stop flag every `check_every` iterations: up to
+    check_every - 1 iterations after the stop rule fired still run their
+    linearise, sweep and line-search launches (these kernels carry no stop
+    guard); their results are discarded by k_mpc_best, which leaves the best
+    iterate, best_du and the control word as they were at the stop."""
     B, n = x_init.shape
     m = C.shape[-1] - n
     dev = x_init.device
@@ -406,9 +423,7 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
             u0 = u0.unsqueeze(1).expand(T, B, m)
         ws.ua.copy_(u0)
     s = N.stream(dev)
-    zI = None if u_zero_I is None else u_zero_I.to(device=dev, dtype=torch.uint8).contiguous()
-    if zI is not None and tuple(zI.shape) != (T, B, m):
-        raise ValueError(f"u_zero_I: expected [T, B, m] = {(T, B, m)}, got {tuple(zI.shape)}")
+    zI = zero_mask(u_zero_I, T, B, m, dev)
     N.call("dilqr_rollout_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f), N.ptr(x_init),
            N.ptr(ws.ua), N.ptr(ws.xa), s)
     for i in range(lqr_iter):

@@ -75,6 +75,30 @@ def test_invalid_arguments_rejected_without_launch():
     assert rc == 1
 
 
+def test_shape_checks_raise_before_launch():
+    """Operands the kernels would index out of bounds (a u_zero_I mask or a
+    grad_input K of the wrong shape) raise ValueError on the host, before any
+    library call."""
+    import torch
+    from dilqr import ops
+    from dilqr.env_dx.cartpole import CartpoleDx
+    T, B, n, m = 4, 3, 5, 1
+    C, c = torch.zeros(T, B, n + m, n + m), torch.zeros(T, B, n + m)
+    F = torch.zeros(T - 1, B, n, n + m)
+    x, u = torch.zeros(T, B, n), torch.zeros(T, B, m)
+    for bad in (torch.zeros(T, m, dtype=torch.bool), torch.zeros(B, m, dtype=torch.bool),
+                torch.zeros(T, B, m + 1, dtype=torch.bool)):
+        with pytest.raises(ValueError, match="u_zero_I"):
+            ops.lqr_backward(C, c, F, n, m, x=x, u=u, u_zero_I=bad)
+        with pytest.raises(ValueError, match="u_zero_I"):
+            ops.lqr_forward(1, torch.zeros(4), torch.zeros(B, n), C, c, x, u, torch.zeros(T, B, m, n),
+                            torch.zeros(T, B, m), u_zero_I=bad)
+    dx = CartpoleDx()
+    for bad in (torch.zeros(T - 1, B, m, n), torch.zeros(B, T, m, n), [torch.zeros(B, m, n)] * (T - 1)):
+        with pytest.raises(ValueError, match="grad_input"):
+            dx.grad_input(x, u, bad)
+
+
 def test_product_path_has_no_cpu_fallback():
     import torch
     import dilqr
