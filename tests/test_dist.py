@@ -1,9 +1,11 @@
 """Multi-process (world_size 2, gloo, CPU) coverage of the batch-sharded path
 that bench.py runs on N GPUs: shard boundaries, the per-shard problem set, the
-max-over-ranks timing reduction, and that solving each shard independently gives
-the same per-problem result as solving the whole batch (so no collective is
-needed in the data path).  The per-shard solver here is the CPU oracle; on the
-GPU box the same shards go through the HIP library."""
+max-over-ranks timing reduction, that solving each shard independently gives
+the same per-problem result as solving the whole batch for fixed-count solves
+(so no collective is needed in the data path), and what a sharded stop-rule
+(eps > 0) solve returns: one reference call per shard.  The
+per-shard solver here is the CPU oracle; on the GPU box the same shards go
+through the HIP library."""
 import os
 import socket
 
@@ -60,6 +62,80 @@ def test_sharded_solve_matches_whole_batch(tmp_path):
                                       not_improved_lim=10 ** 9, linesearch_decay=0.5, max_linesearch_iter=2)
     u_sharded = np.concatenate([np.load(tmp_path / f"u_{r}.npy") for r in range(world)], axis=1)
     np.testing.assert_allclose(u_sharded, u_all, rtol=0, atol=1e-12)
+
+
+STOP_CASE = dict(T=8, B_per=8, seed=3, lqr_iter=40, eps=1e-2, not_improved_lim=5)
+
+
+def _stop_rule_solve(x0, T, lqr_iter, eps, not_improved_lim, q, p):
+    from oracle import models as om
+    from oracle import mpc as ompc
+    C, c = ompc.expand_cost(np.diag(q).astype(np.float64), p.astype(np.float64), T, x0.shape[0])
+    _, u, costs, info = ompc.mpc_forward(om.Cartpole, x0.astype(np.float64), C, c, T, lqr_iter=lqr_iter, eps=eps,
+                                         not_improved_lim=not_improved_lim, linesearch_decay=0.5,
+                                         max_linesearch_iter=2)
+    return u, costs, info["full_du_norm"], info["n_iters"]
+
+
+def _stop_rule_worker(rank, world, port, out_dir):
+    """One rank of a sharded eps > 0 solve: the rank's MPC call over its own
+    contiguous shard, nothing exchanged but the iteration counts (reported)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    k = STOP_CASE
+    B_total = k["B_per"] * world
+    x0_all, q, p = bench.make_problems(B_total, seed=k["seed"])
+    lo, hi = bench.shard_rows(B_total, world, rank)
+    u, costs, du, iters = _stop_rule_solve(x0_all[lo:hi], k["T"], k["lqr_iter"], k["eps"],
+                                           k["not_improved_lim"], q, p)
+    np.savez(os.path.join(out_dir, f"stop_{rank}.npz"), u=u, costs=costs, du=du)
+    its = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(its, torch.tensor([iters]))
+    if rank == 0:
+        np.save(os.path.join(out_dir, "stop_iters.npy"), np.array([int(t.item()) for t in its]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_stop_rule_is_per_shard(tmp_path):
+    """an eps > 0 solve sharded over N ranks is N independent
+    reference MPC calls, one per shard.  The stop rule (mpc_explicit.py:297-299:
+    max full_du_norm < eps or n_not_improved > lim) and the batch-mixing
+    full_du_norm rows (lqr_step_explicit.py:245-247) are evaluated per call, so
+    they are per shard: rank r returns exactly the reference's result for its
+    shard alone, which differs from the whole-batch call wherever the shard's
+    stop fires at another iteration than the whole batch's.  No collective is
+    in the data path."""
+    world = 2
+    k = STOP_CASE
+    mp.spawn(_stop_rule_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    import bench
+    B_total = k["B_per"] * world
+    x0_all, q, p = bench.make_problems(B_total, seed=k["seed"])
+    args = (k["T"], k["lqr_iter"], k["eps"], k["not_improved_lim"], q, p)
+    iters = np.load(tmp_path / "stop_iters.npy")
+    per_shard = []
+    for r in range(world):
+        lo, hi = bench.shard_rows(B_total, world, r)
+        got = np.load(tmp_path / f"stop_{r}.npz")
+        want = _stop_rule_solve(x0_all[lo:hi], *args)
+        for a, b in zip((got["u"], got["costs"], got["du"]), want[:3]):
+            np.testing.assert_array_equal(a, b)          # the rank's result = the call on its shard alone
+        assert iters[r] == want[3]
+        per_shard.append(got)
+    u_w, c_w, du_w, it_w = _stop_rule_solve(x0_all, *args)
+    # this case pins the difference: shard 0 stops with the whole batch (8
+    # iterations), shard 1 one iteration earlier (7)
+    assert list(iters) == [8, 7] and it_w == 8
+    lo, hi = bench.shard_rows(B_total, world, 0)
+    np.testing.assert_array_equal(per_shard[0]["u"], u_w[:, lo:hi])   # same iterations: same iterates
+    np.testing.assert_array_equal(per_shard[0]["costs"], c_w[lo:hi])
+    lo, hi = bench.shard_rows(B_total, world, 1)
+    assert np.abs(per_shard[1]["u"] - u_w[:, lo:hi]).max() > 1e-3    # stopped earlier: a different iterate
+    # best_du is a quirk row of the call's own [T, m, B] buffer: per shard
+    assert not np.array_equal(np.concatenate([s["du"] for s in per_shard]), du_w)
 
 
 def test_shard_rows_cover_batch():
