@@ -94,10 +94,20 @@ inline int grid_group(long long B) { return (int)((B + kGPW - 1) / kGPW); }
     case DILQR_MODEL_PENDULUM: { using MD = Pendulum; CALL; break; } \
     case DILQR_MODEL_CARTPOLE: { using MD = Cartpole; CALL; break; } \
     case DILQR_MODEL_ROCKET: { using MD = Rocket; CALL; break; }     \
+    case DILQR_MODEL_PENDULUM_COMPLEX: { using MD = PendulumComplex; CALL; break; } \
     default: return DILQR_E_SHAPE;                      \
   }
 // models whose Riccati state fits one lane (thread-per-problem kernels)
 #define MODEL_SWITCH_TPP(model, CALL)                   \
+  switch (model) {                                      \
+    case DILQR_MODEL_PENDULUM: { using MD = Pendulum; CALL; break; } \
+    case DILQR_MODEL_CARTPOLE: { using MD = Cartpole; CALL; break; } \
+    case DILQR_MODEL_PENDULUM_COMPLEX: { using MD = PendulumComplex; CALL; break; } \
+    default: return DILQR_E_SHAPE;                      \
+  }
+// ... of those, the models with generated second-order terms (D2Of: the
+// implicit backward, the dynamics VJP)
+#define MODEL_SWITCH_TPP_D2(model, CALL)                \
   switch (model) {                                      \
     case DILQR_MODEL_PENDULUM: { using MD = Pendulum; CALL; break; } \
     case DILQR_MODEL_CARTPOLE: { using MD = Cartpole; CALL; break; } \

@@ -50,11 +50,14 @@ struct IlqrIterArgs {
 int launch_mpc_step_pendulum(const MpcStepArgs& a);
 int launch_mpc_step_cartpole(const MpcStepArgs& a);
 int launch_mpc_step_rocket(const MpcStepArgs& a);
+int launch_mpc_step_pendulum_complex(const MpcStepArgs& a);
 int launch_mpc_solve_pendulum(const MpcSolveArgs& a);
 int launch_mpc_solve_cartpole(const MpcSolveArgs& a);
+int launch_mpc_solve_pendulum_complex(const MpcSolveArgs& a);
 int launch_ilqr_iterate_pendulum(const IlqrIterArgs& a);
 int launch_ilqr_iterate_cartpole(const IlqrIterArgs& a);
 int launch_ilqr_iterate_rocket(const IlqrIterArgs& a);
+int launch_ilqr_iterate_pendulum_complex(const IlqrIterArgs& a);
 
 // rocket implicit backward (dilqr_implicit_group.h)
 struct ImplicitArgs {

@@ -63,6 +63,73 @@ struct Pendulum {
   }
 };
 
+// ---------------------------------------------------------------- pendulum, 5 parameters
+// env_dx/pendulum.py with simple=False (pendulum.py:30-49, 76-95; il_env.py:40-42
+// 'pendulum-complex'): theta = (g, m, l, d, b), a damping d*th and a gravity bias
+// b inside sin(th + b).  The damping needs th itself, so forward() follows the
+// reference's ops: th = atan2(sin, cos), th' = th + dt*dth', cos/sin of th'.
+// The reference has no closed-form Jacobian for this variant (get_linear_dyn
+// and get_matrices unpack three parameters, pendulum.py:157, 448, so its
+// ANALYTIC path fails); its runnable path linearises by autograd
+// (GradMethods.AUTO_DIFF, mpc_explicit.py:547-627), so jacobian() is that
+// derivative: atan2's partials, and the clamp's gate on u (torch.clamp passes
+// the gradient where lo <= u <= hi).
+struct PendulumComplex {
+  static constexpr int N = 3, M = 1, P = 5;
+  static constexpr float DT = 0.05f;
+  static constexpr float ULIM = 2.0f;
+  float kg, ku, dmp, bias;                 // 3g/(2l), 3/(m l^2), d, b
+  DEV void load(const float* __restrict__ th) {
+    const float g = th[0], m = th[1], l = th[2];
+    kg = 3.0f * g / (2.0f * l);
+    ku = 3.0f / (m * (l * l));
+    dmp = th[3];
+    bias = th[4];
+  }
+
+  static constexpr bool kJacFromNext = false;
+  DEV void jacobian_next(const float (&x)[N], const float (&u)[M], const float (&)[N], float (&D)[N][N + M]) const {
+    jacobian(x, u, D);
+  }
+  struct FSparsity {      // every entry of the 3 x 4 Jacobian is a function of the state
+    static constexpr bool nz(int, int) { return true; }
+  };
+
+  template <class S>
+  DEV void forward(const S (&x)[N], const S (&u)[M], S (&o)[N]) const {
+    S uu = vclamp(u[0], -2.0f, 2.0f);
+    S th = vatan2(x[1], x[0]);
+    S newdth = x[2] + DT * ((kg * vsin(th + bias) + ku * uu) - dmp * th);
+    S newth = th + newdth * DT;
+    S sn, cs;
+    vsincos(newth, sn, cs);
+    o[0] = cs; o[1] = sn; o[2] = newdth;
+  }
+
+  DEV void jacobian(const float (&x)[N], const float (&u)[M], float (&D)[N][N + M]) const {
+    const float c = x[0], s = x[1], w = x[2];
+    const float gate = (u[0] >= -2.0f && u[0] <= 2.0f) ? 1.0f : 0.0f;
+    const float uu = fminf(fmaxf(u[0], -2.0f), 2.0f);
+    const float th = atan2f(s, c);
+    float sb, cb;
+    sincosf(th + bias, &sb, &cb);
+    const float newdth = w + DT * ((kg * sb + ku * uu) - dmp * th);
+    float sn, cs;
+    sincosf(th + newdth * DT, &sn, &cs);
+    const float ir2 = 1.0f / (c * c + s * s);
+    const float th_c = -s * ir2, th_s = c * ir2;      // d atan2(s, c)
+    const float a = DT * (kg * cb - dmp);             // d newdth / d th
+    const float nd[4] = {a * th_c, a * th_s, 1.0f, DT * ku * gate};
+    const float nt[4] = {th_c + DT * nd[0], th_s + DT * nd[1], DT, DT * nd[3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      D[0][j] = -sn * nt[j];
+      D[1][j] = cs * nt[j];
+      D[2][j] = nd[j];
+    }
+  }
+};
+
 // ---------------------------------------------------------------- cartpole
 // env_dx/cartpole.py: x = [x, dx, cos th, sin th, dth], u = [force],
 // theta = (g, m_cart, m_pole, l)

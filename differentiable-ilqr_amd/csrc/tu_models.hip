@@ -216,6 +216,7 @@ int dilqr_model_num_ctrl(int model) {
     case DILQR_MODEL_PENDULUM: return Pendulum::M;
     case DILQR_MODEL_CARTPOLE: return Cartpole::M;
     case DILQR_MODEL_ROCKET: return Rocket::M;
+    case DILQR_MODEL_PENDULUM_COMPLEX: return PendulumComplex::M;
     default: return -1;
   }
 }
@@ -225,6 +226,7 @@ int dilqr_model_num_params(int model) {
     case DILQR_MODEL_PENDULUM: return Pendulum::P;
     case DILQR_MODEL_CARTPOLE: return Cartpole::P;
     case DILQR_MODEL_ROCKET: return Rocket::P;
+    case DILQR_MODEL_PENDULUM_COMPLEX: return PendulumComplex::P;
     default: return -1;
   }
 }
@@ -241,7 +243,7 @@ int dilqr_dynamics_vjp_f32(int model, int N, const float* theta, const float* x,
                            float* gtheta, float* gx, float* gu, void* stream) {
   if (N < 0 || !theta || !x || !u || !gout || !gtheta) return DILQR_E_ARG;
   if (N == 0) return 0;
-  MODEL_SWITCH_TPP(model, (k_dynamics_vjp<MD><<<grid_for(N), kBlock, 0, S(stream)>>>(N, theta, x, u, gout, gtheta,
+  MODEL_SWITCH_TPP_D2(model, (k_dynamics_vjp<MD><<<grid_for(N), kBlock, 0, S(stream)>>>(N, theta, x, u, gout, gtheta,
                                                                                        gx, gu)));
   return launched();
 }

@@ -234,6 +234,7 @@ int dilqr_ilqr_iterate_f32(int model, int T, int B, const float* theta, const fl
     case DILQR_MODEL_PENDULUM: return launch_ilqr_iterate_pendulum(a);
     case DILQR_MODEL_CARTPOLE: return launch_ilqr_iterate_cartpole(a);
     case DILQR_MODEL_ROCKET: return launch_ilqr_iterate_rocket(a);
+    case DILQR_MODEL_PENDULUM_COMPLEX: return launch_ilqr_iterate_pendulum_complex(a);
     default: return DILQR_E_SHAPE;
   }
 }
@@ -307,6 +308,7 @@ static int mpc_step(int model, int T, int B, const float* theta, const float* x_
     case DILQR_MODEL_PENDULUM: return launch_mpc_step_pendulum(a);
     case DILQR_MODEL_CARTPOLE: return launch_mpc_step_cartpole(a);
     case DILQR_MODEL_ROCKET: return launch_mpc_step_rocket(a);
+    case DILQR_MODEL_PENDULUM_COMPLEX: return launch_mpc_step_pendulum_complex(a);
     default: return DILQR_E_SHAPE;
   }
 }
@@ -345,10 +347,11 @@ int dilqr_mpc_solve_fixed_f32(int model, int T, int B, const float* theta, const
   if (m < 1) return DILQR_E_SHAPE;
   if (B == 0) return 0;
   int e;
-  if (model == DILQR_MODEL_PENDULUM || model == DILQR_MODEL_CARTPOLE) {
+  if (model == DILQR_MODEL_PENDULUM || model == DILQR_MODEL_CARTPOLE || model == DILQR_MODEL_PENDULUM_COMPLEX) {
     const MpcSolveArgs a{T, B, theta, x_init, u_init, C, c, mkb(bounds), linesearch_decay, max_linesearch_iter,
                          iterations, best_cost_eps, st, S(stream)};
-    e = model == DILQR_MODEL_CARTPOLE ? launch_mpc_solve_cartpole(a) : launch_mpc_solve_pendulum(a);
+    e = model == DILQR_MODEL_CARTPOLE ? launch_mpc_solve_cartpole(a)
+        : model == DILQR_MODEL_PENDULUM ? launch_mpc_solve_pendulum(a) : launch_mpc_solve_pendulum_complex(a);
   } else {
     // the 16-lanes-per-problem models change their lane mapping between the
     // sweep and the line search: one launch pair per iteration

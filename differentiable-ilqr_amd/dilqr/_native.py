@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("DILQR_LIB", os.path.join(_HERE, "libdilqr.so"))
 ABI_VERSION = 7
 _PKG = os.path.dirname(_HERE)          # differentiable-ilqr_amd/ (the Makefile's directory)
 
-MODEL_LINDX, MODEL_PENDULUM, MODEL_CARTPOLE, MODEL_ROCKET = 0, 1, 2, 3
+MODEL_LINDX, MODEL_PENDULUM, MODEL_CARTPOLE, MODEL_ROCKET, MODEL_PENDULUM_COMPLEX = 0, 1, 2, 3, 4
 BOUNDS_NONE, BOUNDS_SCALAR, BOUNDS_TENSOR = 0, 1, 2
 SOLVE_INV, SOLVE_CHOL = 0, 1
 ERRORS = {1: "unsupported shape/model", 2: "invalid argument", 3: "unsupported option combination"}

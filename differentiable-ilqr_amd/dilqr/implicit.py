@@ -12,6 +12,10 @@ def implicit_backward(model, dl_dx, dl_du, C, c, F, f, x, u, K, u_lower, u_upper
     gains in natural time order (the kernel applies the reference's reversed
     stacking).  F, f are not needed: the kernel re-linearises at (x, u)."""
     mid = ops.model_id_of(model)
+    if mid == N.MODEL_PENDULUM_COMPLEX:
+        raise NotImplementedError(
+            "dilqr: no implicit backward for the 5-parameter pendulum: the reference's grad_input / get_matrices "
+            "exist for the 3-parameter model only (pendulum.py:157 unpacks g, m, l)")
     if mid not in (N.MODEL_CARTPOLE, N.MODEL_PENDULUM, N.MODEL_ROCKET):
         raise NotImplementedError("dilqr: the implicit backward needs a pendulum, cartpole or rocket model")
     T, B, n = x.shape

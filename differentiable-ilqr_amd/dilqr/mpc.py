@@ -50,8 +50,9 @@ class MPC(Module):
     def fused(self, cost, dx):
         """The device-resident loop: env_dx model (ANALYTIC) or LinDx, quadratic
         cost, no slew-rate penalty / delta_u; anything else -> dilqr.generic."""
-        model_ok = isinstance(dx, LinDx) or (getattr(dx, "model_id", None) is not None
-                                             and self.grad_method == GradMethods.ANALYTIC)
+        model_ok = isinstance(dx, LinDx) or (getattr(dx, "model_id", None) is not None and (
+            self.grad_method == GradMethods.ANALYTIC
+            or (self.grad_method == GradMethods.AUTO_DIFF and getattr(dx, "jacobian_is_autograd", False))))
         return isinstance(cost, QuadCost) and model_ok and self.slew_rate_penalty is None and self.delta_u is None
 
     def forward(self, x_init, cost, dx):

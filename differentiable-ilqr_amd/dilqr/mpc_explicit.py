@@ -78,10 +78,13 @@ class MPC(Module):
         """The whole loop on device in HIP kernels: an env_dx model with its
         analytic Jacobian, a quadratic cost, no slew-rate penalty / delta_u
         (the fused iteration; with a u_zero_I mask the unfused kernels).
-        Anything else runs the generic loop (dilqr.generic)."""
-        return (isinstance(cost, QuadCost) and getattr(dx, "model_id", None) is not None
-                and self.grad_method == GradMethods.ANALYTIC and self.slew_rate_penalty is None
-                and self.delta_u is None)
+        AUTO_DIFF takes the same path for a model whose Jacobian is the autograd
+        one (the 5-parameter pendulum).  Anything else runs the generic loop
+        (dilqr.generic)."""
+        jac_ok = self.grad_method == GradMethods.ANALYTIC or (
+            self.grad_method == GradMethods.AUTO_DIFF and getattr(dx, "jacobian_is_autograd", False))
+        return (isinstance(cost, QuadCost) and getattr(dx, "model_id", None) is not None and jac_ok
+                and self.slew_rate_penalty is None and self.delta_u is None)
 
     def forward(self, x_init, cost, dx):
         if not x_init.is_cuda:

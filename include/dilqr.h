@@ -43,6 +43,12 @@ extern "C" {
 #define DILQR_MODEL_PENDULUM 1   /* env_dx/pendulum.py   n=3  m=1 p=3            */
 #define DILQR_MODEL_CARTPOLE 2   /* env_dx/cartpole.py   n=5  m=1 p=4            */
 #define DILQR_MODEL_ROCKET 3     /* env_dx/rocket.py     n=13 m=3 p=5            */
+#define DILQR_MODEL_PENDULUM_COMPLEX 4  /* env_dx/pendulum.py simple=False: n=3 m=1
+                                    p=5 (g, m, l, damping, gravity bias); its
+                                    Jacobian is the autograd one (the clamp's
+                                    gate applied), no second-order terms: the
+                                    implicit backward, get_matrices, grad_input
+                                    and the dynamics VJP return DILQR_E_SHAPE */
 
 /* ---- control bounds (MPC u_lower/u_upper: float or [T,B,m] tensor) -------- */
 #define DILQR_BOUNDS_NONE 0

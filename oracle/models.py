@@ -173,6 +173,62 @@ class Pendulum(_Model):
         return q, p
 
 
+class PendulumComplex(_Model):
+    """env_dx/pendulum.py with simple=False (pendulum.py:30-49, 76-95): theta =
+    (g, m, l, d, b), damping d*th and a gravity bias inside sin(th + b).  The
+    reference has no closed-form Jacobian for it (get_linear_dyn unpacks three
+    parameters, pendulum.py:448); its runnable linearisation is AUTO_DIFF
+    (mpc_explicit.py:562-566), i.e. autograd through forward(): the clamp's gate
+    on u included.  get_linear_dyn here is that derivative."""
+    name = "pendulum_complex"
+    n_state, n_ctrl, n_params = 3, 1, 5
+    default_params = (10.0, 1.0, 1.0, 1.0, 0.1)     # il_env.py:41
+    dt = 0.05
+    max_torque = 2.0
+    lower, upper = -2.0, 2.0
+    mpc_eps, linesearch_decay, max_linesearch_iter = 1e-3, 0.2, 5
+
+    @classmethod
+    def forward(cls, x, u, params=None):
+        """pendulum.py:76-95 (simple=False branch)."""
+        g, m, l, d, b = (x.dtype.type(v) for v in (params if params is not None else cls.default_params))
+        dt = x.dtype.type(cls.dt)
+        uu = np.clip(u, -cls.max_torque, cls.max_torque)[:, 0]
+        c, s, dth = x[:, 0], x[:, 1], x[:, 2]
+        th = np.arctan2(s, c)
+        newdth = dth + dt * (-3. * g / (2. * l) * (-np.sin(th + b)) + 3. * uu / (m * l ** 2) - d * th)
+        newth = th + newdth * dt
+        return np.stack([np.cos(newth), np.sin(newth), newdth], 1)
+
+    @classmethod
+    def _sym_next_state(cls, xs, us, ps):
+        c, s, dth = xs
+        (u,) = us
+        g, m, l, d, b = ps
+        th = sp.atan2(s, c)
+        newdth = dth + sp.Float(cls.dt) * (3 * g / (2 * l) * sp.sin(th + b) + 3 * u / (m * l ** 2) - d * th)
+        newth = th + newdth * sp.Float(cls.dt)
+        return [sp.cos(newth), sp.sin(newth), newdth]
+
+    @classmethod
+    def get_linear_dyn(cls, x, u, params=None):
+        """Autograd's Jacobian of forward(): the symbolic one at the clamped u,
+        its u column gated by lo <= u <= hi (torch.clamp's backward)."""
+        uc = np.clip(u, cls.lower, cls.upper)
+        D = cls._eval("D", x, uc, params, (cls.n_state, cls.n_state + cls.n_ctrl))
+        gate = ((u >= cls.lower) & (u <= cls.upper)).astype(x.dtype)          # [N, m]
+        D[:, :, cls.n_state:] *= gate[:, None, :]
+        return D
+
+    @classmethod
+    def get_matrices(cls, x, u, params=None):
+        raise NotImplementedError("the reference's get_matrices has no 5-parameter form (pendulum.py:157)")
+
+    @classmethod
+    def true_obj(cls):
+        return Pendulum.true_obj()
+
+
 class Cartpole(_Model):
     """env_dx/cartpole.py, n=5 [x, dx, cos th, sin th, dth], m=1."""
     name = "cartpole"
@@ -451,4 +507,4 @@ class Rocket(_Model):
         return q, p
 
 
-MODELS = {"pendulum": Pendulum, "cartpole": Cartpole, "rocket": Rocket}
+MODELS = {"pendulum": Pendulum, "cartpole": Cartpole, "rocket": Rocket, "pendulum_complex": PendulumComplex}

@@ -717,12 +717,57 @@ def case_api():
         save(f"api_{tname(dt)}", **out)
 
 
+# --------------------------------------------------------------------------
+# L. the 5-parameter pendulum (pendulum.py simple=False, il_env.py:40-42
+#    'pendulum-complex'): forward, its autograd Jacobian (the reference's own
+#    closed forms unpack three parameters and fail for it), and MPC solves
+#    through mpc_explicit.MPC with GradMethods.AUTO_DIFF, the runnable path
+# --------------------------------------------------------------------------
+COMPLEX_PARAMS = (10., 1., 1., 1.0, 0.1)        # il_env.py:41
+COMPLEX_MPC = {
+    # name: (T, B, lqr_iter, eps, not_improved_lim)  bounds +-2, decay 0.2, max_ls 5 (pendulum.py:52-58)
+    "fixed": (20, 16, 10, 0.0, 10 ** 9),
+    "il": (20, 16, 40, 1e-3, 5),
+}
+
+
+def case_complex():
+    print("L. pendulum-complex")
+    for dt in (torch.float64, torch.float32):
+        with default_dtype(dt):
+            out = {}
+            dxm = R.pendulum.PendulumDx(torch.tensor(COMPLEX_PARAMS, dtype=dt), simple=False)
+            rng = np.random.RandomState(21)
+            x, u = sample_states("pendulum", 256, rng)
+            X = torch.tensor(x, dtype=dt, requires_grad=True)
+            U = torch.tensor(u, dtype=dt, requires_grad=True)
+            nx = dxm(X, U)
+            rows = [torch.autograd.grad(nx[:, j].sum(), [X, U], retain_graph=True) for j in range(3)]
+            D = torch.stack([torch.cat(r, 1) for r in rows], 1)          # [N, n, d], as AUTO_DIFF forms it
+            out.update(x=x, u=u, fwd=np_(nx), jac=np_(D))
+            for name, (T, B, it, eps, nil) in COMPLEX_MPC.items():
+                rng = np.random.RandomState(3)
+                x0 = xinit_for("pendulum", B, rng)
+                Q, P = true_cost(dxm, T, B, dt)
+                m = R.mpc_explicit.MPC(3, 1, T, u_lower=-2.0, u_upper=2.0, lqr_iter=it, eps=eps,
+                                       not_improved_lim=nil, linesearch_decay=0.2, max_linesearch_iter=5,
+                                       exit_unconverged=False, detach_unconverged=False, verbose=-1,
+                                       grad_method=R.mpc_explicit.GradMethods.AUTO_DIFF)
+                # AUTO_DIFF differentiates the dynamics with torch.autograd.grad
+                # (mpc_explicit.py:562-566): grad mode stays on
+                with contextlib.redirect_stdout(io.StringIO()):
+                    xs, us, costs = m(torch.tensor(x0, dtype=dt), R.mpc_explicit.QuadCost(Q, P), dxm)
+                out.update({f"{name}_x0": x0, f"{name}_x": np_(xs), f"{name}_u": np_(us),
+                            f"{name}_costs": np_(costs)})
+            save(f"complex_{tname(dt)}", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["models", "riccati", "pnqp", "lqrstep", "mpc", "adjoint", "implicit",
-                             "datasets", "il", "generic", "api"]
+                             "datasets", "il", "generic", "api", "complex"]
     table = {"models": case_models, "riccati": case_riccati, "pnqp": case_pnqp,
              "lqrstep": case_lqrstep, "mpc": case_mpc, "adjoint": case_classic_adjoint,
              "implicit": case_implicit, "datasets": case_datasets, "il": case_il,
-             "generic": case_generic, "api": case_api}
+             "generic": case_generic, "api": case_api, "complex": case_complex}
     for w in which:
         table[w]()

@@ -44,7 +44,9 @@ def dilqr_models():
     from dilqr.env_dx.cartpole import CartpoleDx
     from dilqr.env_dx.pendulum import PendulumDx
     from dilqr.env_dx.rocket import RocketDx
-    return {"cartpole": CartpoleDx, "pendulum": PendulumDx, "rocket": RocketDx}
+    return {"cartpole": CartpoleDx, "pendulum": PendulumDx, "rocket": RocketDx,
+            "pendulum_complex": lambda: PendulumDx(torch.tensor(omodels.PendulumComplex.default_params),
+                                                   simple=False)}
 
 
 # ------------------------------------------------------------------ dynamics
@@ -57,6 +59,18 @@ def test_dynamics_and_jacobian(golden, name):
     D = cpu(dx.get_linear_dyn(gpu(x), gpu(u)))
     assert relerr(out, g[f"{name}_fwd"]) < 2e-5
     assert relerr(D, g[f"{name}_D"]) < 5e-5
+
+
+def test_pendulum_complex_dynamics_and_jacobian(golden):
+    """The 5-parameter pendulum (pendulum.py simple=False) against the
+    reference's forward and the autograd Jacobian its AUTO_DIFF path forms."""
+    g = golden("complex_f64")
+    dx = dilqr_models()["pendulum_complex"]()
+    out = cpu(dx(gpu(g["x"]), gpu(g["u"])))
+    D = cpu(dx.get_linear_dyn(gpu(g["x"]), gpu(g["u"])))
+    e_f, e_d = relerr(out, g["fwd"]), relerr(D, g["jac"])
+    print(f"\n[pendulum-complex] forward {e_f:.2e}, Jacobian {e_d:.2e}")
+    assert e_f < 2e-5 and e_d < 5e-5
 
 
 # ------------------------------------------------------------------ Riccati
@@ -300,6 +314,61 @@ def test_mpc_solve_vs_oracle(golden, name):
     rerr = np.abs(cpu(costs) - ref) / np.maximum(1.0, np.abs(ref))
     print(f"[{name}] vs the reference's fp64 costs: max rel {rerr.max():.2e}, median {np.median(rerr):.2e}")
     assert np.max(rerr) < 1e-4, np.max(rerr)
+
+
+COMPLEX_MPC = {"fixed": (20, 10, 0.0, 10 ** 9), "il": (20, 40, 1e-3, 5)}     # T, lqr_iter, eps, not_improved_lim
+
+
+@pytest.mark.parametrize("name", list(COMPLEX_MPC))
+def test_pendulum_complex_mpc_vs_golden(golden, name):
+    """MPC solves of the 5-parameter pendulum (bounds +-2, decay 0.2, max_ls 5,
+    the IL settings of pendulum.py:52-58) on the fused HIP iteration: by
+    decision replay against the fp64 oracle, and against the reference's own
+    fp64 solve (mpc_explicit.MPC with GradMethods.AUTO_DIFF, the path that runs
+    for this model).  dilqr.MPC takes the same kernels with ANALYTIC and with
+    AUTO_DIFF (its Jacobian is the autograd one): identical bits."""
+    import dilqr
+    g = golden("complex_f64")
+    T, it, eps, nil = COMPLEX_MPC[name]
+    x0 = g[f"{name}_x0"]
+    x, u, costs, alphas, takes = gpu_solve_with_decisions(x0, "pendulum_complex", T, it, (-2.0, 2.0), eps, nil,
+                                                          0.2, 5)
+    x2, u2, c2 = run_gpu_mpc(x0, "pendulum_complex", T, it, (-2.0, 2.0), eps, nil, 0.2, 5)
+    assert same_bits(x, x2) and same_bits(u, u2) and same_bits(costs, c2)
+    dx = dilqr_models()["pendulum_complex"]()
+    q, p = dx.get_true_obj()
+    B = x0.shape[0]
+    m = dilqr.MPC(3, 1, T, u_lower=-2.0, u_upper=2.0, lqr_iter=it, eps=eps, not_improved_lim=nil,
+                  linesearch_decay=0.2, max_linesearch_iter=5, exit_unconverged=False, detach_unconverged=False,
+                  grad_method=dilqr.GradMethods.AUTO_DIFF)
+    with torch.no_grad():
+        x3, u3, c3 = m(gpu(x0), dilqr.QuadCost(torch.diag(q).repeat(T, B, 1, 1).to(DEV), p.repeat(T, B, 1).to(DEV)),
+                       dx)
+    assert same_bits(u, u3) and same_bits(costs, c3)
+    check_against_forced_oracle(omodels.PendulumComplex, x0, T, (-2.0, 2.0), 0.2, 5, x, u, costs, alphas, takes,
+                                f"complex_{name}")
+    ref = g[f"{name}_costs"]
+    rerr = np.abs(cpu(costs) - ref) / np.maximum(1.0, np.abs(ref))
+    print(f"[complex_{name}] vs the reference's fp64 costs: max rel {rerr.max():.2e}")
+    assert np.max(rerr) < 1e-4, np.max(rerr)
+
+
+def test_pendulum_complex_backward_refused():
+    """No implicit backward for the 5-parameter pendulum (the reference's
+    grad_input has no 5-parameter form, pendulum.py:157): a solve whose inputs
+    carry gradients solves, and its backward raises instead of returning
+    silently wrong gradients."""
+    import dilqr
+    dx = dilqr_models()["pendulum_complex"]()
+    dx.params = dx.params.clone().to(DEV).requires_grad_(True)
+    T, B = 5, 4
+    q, p = dx.get_true_obj()
+    m = dilqr.MPC(3, 1, T, u_lower=-2.0, u_upper=2.0, lqr_iter=3, exit_unconverged=False,
+                  detach_unconverged=False)
+    x, u, _ = m(gpu(np.tile([1.0, 0.0, 0.0], (B, 1))),
+                dilqr.QuadCost(torch.diag(q).repeat(T, B, 1, 1).to(DEV), p.repeat(T, B, 1).to(DEV)), dx)
+    with pytest.raises(NotImplementedError, match="5-parameter"):
+        u.sum().backward()
 
 
 def same_bits(a, b):

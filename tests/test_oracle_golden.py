@@ -169,6 +169,35 @@ def test_mpc_f32(golden, name):
     assert np.max(np.abs(costs - ref) / np.maximum(1.0, np.abs(ref))) < 1e-3
 
 
+# ---------------------------------------------------------------- 5-parameter pendulum
+@pytest.mark.parametrize("prec,tol", [("f64", 1e-12), ("f32", 2e-5)])
+def test_pendulum_complex_forward_and_jacobian(golden, prec, tol):
+    """pendulum.py simple=False: forward and its autograd Jacobian (the
+    reference's AUTO_DIFF linearisation, mpc_explicit.py:562-566)."""
+    g = golden(f"complex_{prec}")
+    dt = np.float64 if prec == "f64" else np.float32
+    x, u = g["x"].astype(dt), g["u"].astype(dt)
+    PC = models.PendulumComplex
+    assert rel(PC.forward(x, u), g["fwd"]) < tol
+    assert rel(PC.get_linear_dyn(x, u), g["jac"]) < 10 * tol
+
+
+@pytest.mark.parametrize("name", ["fixed", "il"])
+def test_pendulum_complex_mpc_f64(golden, name):
+    """mpc_explicit.MPC(GradMethods.AUTO_DIFF) on the 5-parameter pendulum,
+    bounds +-2, decay 0.2, max_ls 5 (the reference's fp64 run)."""
+    g = golden("complex_f64")
+    T, B = g[f"{name}_u"].shape[:2]
+    it, eps, nil = {"fixed": (10, 0.0, 10 ** 9), "il": (40, 1e-3, 5)}[name]
+    q, p = models.PendulumComplex.true_obj()
+    C, c = mpc.expand_cost(np.diag(q), p, T, B)
+    x, u, costs, _ = mpc.mpc_forward(models.PendulumComplex, g[f"{name}_x0"], C, c, T, u_lower=-2.0, u_upper=2.0,
+                                     lqr_iter=it, eps=eps, not_improved_lim=nil, linesearch_decay=0.2,
+                                     max_linesearch_iter=5)
+    assert rel(u, g[f"{name}_u"]) < 1e-8 and rel(x, g[f"{name}_x"]) < 1e-8
+    assert rel(costs, g[f"{name}_costs"]) < 1e-8
+
+
 # ---------------------------------------------------------------- classic adjoint
 @pytest.mark.parametrize("tag,bounds", [("m1", None), ("m3", None), ("m1box", (-0.5, 0.5)),
                                         ("m3box", (-0.5, 0.5))])
