@@ -55,10 +55,11 @@ def iter_cost_floats(flags, T=T_HORIZON, d=D):
     pk = d * (d + 1) // 2 + d
     f = np.asarray(flags).astype(np.int64)
     out = np.full(f.shape, T * (d * d + d), np.float64)                    # asymmetric: the caller's C, c
-    out[(f & 1) != 0] = T * pk                                              # packed symmetric
-    out[(f & 5) == 5] = pk                                                  # ... time-invariant: one record
-    out[(f & 3) == 3] = T * 2 * d                                           # diagonal: diag(C_t), c_t
-    out[(f & 7) == 7] = 2 * d                                               # ... time-invariant: in registers
+    if d <= 8:                                                              # packed copies: one-lane models
+        out[(f & 1) != 0] = T * pk                                          # packed symmetric
+        out[(f & 5) == 5] = pk                                              # ... time-invariant: one record
+        out[(f & 3) == 3] = T * 2 * d                                       # diagonal: diag(C_t), c_t
+    out[(f & 7) == 7] = 2 * d                                               # time-invariant diagonal: registers
     return out
 
 
@@ -299,12 +300,39 @@ def implicit_kernel_ms(dx, wx, wu, C, c, x, u, K, lo, hi, dev, reps=5):
     return ms
 
 
-def flop_roofline(kernel, flops, ms, B, T, bounds):
+def implicit_boundary_bytes(n, m, T, B):
+    """Bytes the implicit backward must move per launch: C, c, x, u, K (the
+    gains of the no-op forward), dl/dx, dl/du in; dC, dc out (dtheta, B*p floats,
+    and theta are negligible).  Its private workspace (the modified Riccati
+    gains B -> C and the rollout y C -> D) is not counted."""
+    d = n + m
+    return 4 * T * B * (d * d + d + n + m + m * n + n + m + d * d + d)
+
+
+def implicit_roofline(kernel, flops, nbytes, ms, B, T, bounds, pmc_sig):
+    """Both rooflines of an implicit backward launch: fp32 vector flops and HBM
+    (boundary bytes), with the PMC counters of the same instantiation; `bound`
+    names the limiter the counters show (waitcnt stall vs VALU busy)."""
     tf = flops / (ms * 1e-3) / 1e12
-    return {"kernel": kernel, "bound": "valu", "avg_ms": ms, "problems_per_s": B / (ms * 1e-3), "batch": B, "T": T,
-            "bounds": bounds, "flops_per_launch": flops, "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": tf / FP32_PEAK_TFLOPS,
-            "flops_source": "profiles/implicit_flops.json (counted per problem, tools/implicit_flops.py)"}
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    e = with_pmc({"kernel": kernel, "avg_ms": ms, "problems_per_s": B / (ms * 1e-3), "batch": B, "T": T,
+                  "bounds": bounds, "unit": "GB/s", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                  "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": nbytes,
+                  "bytes_model": "boundary bytes: C, c, x, u, K, dl/dx, dl/du in; dC, dc out",
+                  "flops": {"flops_per_launch": flops, "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "frac": tf / FP32_PEAK_TFLOPS,
+                            "source": "profiles/implicit_flops.json (counted per problem, tools/implicit_flops.py)"}},
+                 pmc_sig)
+    pm = e.get("pmc", {})
+    if "valu_busy" in pm and "waitcnt_stall" in pm:
+        e["bound"] = "hbm" if pm["waitcnt_stall"] > pm["valu_busy"] else "valu"
+        e["limiter"] = (f"PMC: waitcnt stall {pm['waitcnt_stall']:.2f} vs VALU busy {pm['valu_busy']:.2f} of wave "
+                        f"cycles")
+    else:
+        e["bound"] = "hbm"
+    if e.get("traffic"):
+        e["traffic_over_boundary"] = e["traffic"] / nbytes
+    return e
 
 
 def rocket_problems(B, dev):
@@ -358,7 +386,15 @@ def secondary_configs(dev):
     # sweep (16 lanes per problem) and the line search (one problem per lane)
     it_ms = steady_iteration_ms(ops.MPCSolve(T, B, n, m, dev), N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, dev)
     d = n + m
-    it_bytes = 4 * (T * d * d + T * d + n + 2 * T * d + 2) * B                 # 36,540 B/problem, SURVEY §8(d)
+    # bytes of one steady iteration as the kernels move them (counted the way
+    # iter_cost_floats counts cartpole): the cost as the register-cost kernels
+    # read it (a time-invariant diagonal one: 2d floats), x_init, the current
+    # trajectory in and the new one out, cost and du_norm, plus the gain
+    # records (K_t, k_t: m*n + m floats per step) the group sweep hands the
+    # lane-pair search through HBM (written once, read once)
+    cf = iter_cost_floats(sv.cost_sym.cpu().numpy(), T=T, d=d)
+    it_bytes = float((iter_bytes_per_problem(cf, T=T, n=n, d=d) + 4 * 2 * T * (m * n + m)).sum())
+    survey_bytes = 4 * (T * d * d + T * d + n + 2 * T * d + 2) * B             # 36,540 B/problem, SURVEY §8(d)
     gbs = it_bytes / (it_ms * 1e-3) / 1e9
     out["config3_rocket"] = {
         "value": val, "unit": "problem-iters/s", "ms_per_iter": ms_it, "batch": B, "T": T,
@@ -367,6 +403,11 @@ def secondary_configs(dev):
                        "dense-cost instantiation, which leaves at once): one MPC iteration of the timed solves, "
                        "steady state",
              "bound": "hbm", "avg_launch_ms": it_ms, "algorithmic_bytes_per_launch": it_bytes,
+             "bytes_model": "cost as read (time-invariant diagonal: 2d floats in registers) + x_init + tau in/out "
+                            "+ cost, du_norm + gain records through HBM (2 T (mn+m) floats)",
+             "survey_bytes_per_launch": survey_bytes,
+             "survey_bytes_note": "SURVEY.md §8(d) 36,540 B/problem counts the caller's C at every step, which the "
+                                  "steady kernels never read (not a roofline figure)",
              "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
             ("k_mpc_sweep_group<Rocket, 0>", "k_mpc_search_lane<Rocket, 0, true>",
              "k_mpc_search_lane<Rocket, 0, false>")),
@@ -380,9 +421,9 @@ def secondary_configs(dev):
     wu = torch.randn(T, B, m, device=dev, generator=g)                 # loss = sum(u * w), SURVEY §8(d)
     implicit_backward(dx, wx, wu, C, c, None, None, x, u, K, None, None, None)      # the autograd path runs
     ms = implicit_kernel_ms(dx, wx, wu, C, c, x, u, K, None, None, dev)
-    out["config3_rocket"]["implicit_backward"] = with_pmc(flop_roofline(
-        "k_implicit_backward_group<Rocket> (dC, dc, dtheta)", implicit_flops_per_problem("rocket", T) * B, ms, B,
-        T, "none"), "k_implicit_backward_group<Rocket, RocketD2, 0>")
+    out["config3_rocket"]["implicit_backward"] = implicit_roofline(
+        "k_implicit_backward_group<Rocket> (dC, dc, dtheta)", implicit_flops_per_problem("rocket", T) * B,
+        implicit_boundary_bytes(n, m, T, B), ms, B, T, "none", "k_implicit_backward_group<Rocket, RocketD2, 0>")
     del sv, C, c, x0, x, u, F, K, wx, wu
     # ---- config 4: cartpole T=25 B=65536 with bounds (+-100 reference value, +-10 stress) + implicit backward
     T, B, n, m = 25, 65536, 5, 1
@@ -427,9 +468,9 @@ def secondary_configs(dev):
     cart = CartpoleDx()
     implicit_backward(cart, wx, wu, C, c, None, None, x, u, K, -10.0, 10.0, None)
     ms = implicit_kernel_ms(cart, wx, wu, C, c, x, u, K, -10.0, 10.0, dev)
-    out["config4_implicit_backward"] = with_pmc(flop_roofline(
-        "k_implicit_backward<Cartpole> (dC, dc, dtheta)", implicit_flops_per_problem("cartpole", T) * B, ms, B, T,
-        "+-10"), "k_implicit_backward<Cartpole>")
+    out["config4_implicit_backward"] = implicit_roofline(
+        "k_implicit_backward<Cartpole> (dC, dc, dtheta)", implicit_flops_per_problem("cartpole", T) * B,
+        implicit_boundary_bytes(n, m, T, B), ms, B, T, "+-10", "k_implicit_backward<Cartpole>")
     del sv, C, c
     # ---- one empc training step of the IL loop (il_exp.py:297-352):
     # MPC forward (lqr_iter 100, eps 1e-4, bounds +-100, T=35) + im_loss backward into the

@@ -19,11 +19,12 @@ namespace dilqr {
 constexpr int kG = 16;          // lanes per problem
 constexpr int kGPW = 64 / kG;   // problems per wave (= per workgroup)
 // Occupancy floor of the implicit group kernel (waves per SIMD, i.e. at most
-// 512/N VGPRs): left alone the compiler gives it 185 VGPRs = 2 waves per SIMD;
-// 3 measured 2.38 ms vs 2.43 at config 3, while 4 spills (4.4 ms).  The fused
-// iteration is fastest without a floor (175 VGPRs).
+// 512/N VGPRs).  Round 4's pass D (the costates recomputed, the gradx adjoint
+// carried down, ws records of 64 floats instead of 160) needs 205 VGPRs: at a
+// floor of 3 (168) it spills ~130 VGPRs, at 2 it spills none — and config 3
+// (B = 32768: 2048 waves) has two waves per SIMD to give anyway.
 #ifndef DILQR_GROUP_WAVES
-#define DILQR_GROUP_WAVES 3
+#define DILQR_GROUP_WAVES 2
 #endif
 constexpr int kGroupWavesPerSimd = DILQR_GROUP_WAVES;
 

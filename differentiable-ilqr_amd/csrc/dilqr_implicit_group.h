@@ -2,7 +2,7 @@
 // tu_implicit.hip) for the 16-lanes-per-problem models (rocket, d = 16).
 // Included by tu_implicit_rocket.hip after dilqr_group.h.
 //
-// Same three passes (B down, A+C up, D down) and the same algebra as the one-lane kernel
+// Same three passes (B down, C up, D down) and the same algebra as the one-lane kernel
 // (oracle/adjoint.py implicit_backward_fast; lqr_step_explicit.py:653-712 with
 // rocket's grad_input, rocket.py:263-323, and its build_batched_* tables,
 // rocket.py:541-820), distributed by rows: lane r owns row r of every d x d or
@@ -13,7 +13,7 @@
 //   xx_row(r) row r of the reference's x_grad_xtm1 builder
 //   xth_row(r) row r of dx_{t+1}/dtheta
 // and Model::jac_row(r) (row r of D_t, which is also x_grad_utm1's source).
-// Vectors every lane needs in full (gradx, lam, dlam, y) go through LDS; the
+// Vectors every lane needs in full (lam, dlam, y, the adjoint carry) go through LDS; the
 // Riccati step of the modified problem is group_riccati_step.
 #pragma once
 
@@ -21,25 +21,25 @@
 
 namespace dilqr {
 
-// per-(t,b) workspace record (floats), written lane-contiguous
+// per-(t,b) workspace record (floats), written lane-contiguous: what pass C
+// and pass D cannot recompute — the modified Riccati step's gains (B -> C) and
+// the rollout y (C -> D).  The costates are recomputed by pass D and gradx is
+// replaced by its adjoint (tu_implicit.hip), so neither is stored.
 template <class Model> struct ImplicitGroupWs {
   static constexpr int n = Model::N, m = Model::M, p = Model::P;
-  static constexpr int GX = 0;                 // gradx_t, [p][16] (lane r < n: row r)
-  static constexpr int LAM = GX + p * kG;      // lam_t, [16]
-  static constexpr int KG = LAM + kG;          // [m][16]: K[a][r] at r < n, k[a] at n
+  static constexpr int KG = 0;                 // [m][16]: K[a][r] at r < n, k[a] at n
   static constexpr int Y = KG + m * kG;        // y_t, [16]
   static constexpr int REC = Y + kG;
 };
 
 template <int n, int p>
 struct ImplicitGroupLds {
-  float gx[n][p + 1];                          // gradx_{t-1} (phase A)
-  float vec[kG];                               // lam_{t+1} (B) / y_t (C, D)
-  // dlam_{t+1} (D); the tail makes the struct an odd number of words mod 32,
-  // so the gx rows of a half-wave's two groups (stride p+1 words) fall on
-  // disjoint banks
-  static constexpr int kWords = n * (p + 1) + 2 * kG;
-  float dlam[kG + ((kWords % 2) ? 0 : 1)];
+  // rows of the gradx-adjoint carry: row i = mu_i * x_grad_xtm1[i][:] (lane i
+  // writes its row, lane l sums column l); odd row stride for the column reads
+  float ax[n][n + 2];
+  float vec[kG];                               // lam_{t+1} (B) / y_t (C)
+  float lam[kG];                               // lam_{t+1} (D)
+  float dlam[kG];                              // dlam_{t+1} (D)
 };
 
 template <class Model, class D2, int MODE>
@@ -73,6 +73,13 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
 #pragma unroll
     for (int a = 0; a < m; ++a) ut[a] = u[tb * m + a];
   };
+  // Pass B also tests, per lane, whether row r of C_t is the same diagonal row
+  // for every t (off-diagonal words +0.0, the diagonal equal to step T-1's bit
+  // for bit) and whether c_t[r] is: pass D then takes them from registers (the
+  // reference's callers pass diag(q), p repeated over t; the same values, so
+  // the same arithmetic, and C is read once instead of twice).
+  float cdg = 0.f, cvr = 0.f;
+  unsigned c_offd = 0u, c_dif = 0u, cv_dif = 0u;
   // ---------------- B: costates, M_t, Riccati of the C + M^T problem (active set masked)
   {
     if (r < n) {
@@ -98,6 +105,15 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         cr = c[tb * d + r];
         gr = r < n ? dl_dx[tb * n + r] : dl_du[tb * m + (r - n)];
       }
+      float cdr = 0.f;
+#pragma unroll
+      for (int j = 0; j < d; ++j) {
+        cdr = (j == r) ? Crow[j] : cdr;
+        if (j != r) c_offd |= __float_as_uint(Crow[j]);
+      }
+      if (t == T - 1) { cdg = cdr; cvr = cr; }
+      c_dif |= __float_as_uint(cdr) ^ __float_as_uint(cdg);
+      cv_dif |= __float_as_uint(cr) ^ __float_as_uint(cvr);
       float lam1[n];
 #pragma unroll
       for (int i = 0; i < n; ++i) lam1[i] = I.vec[i];     // lam_{t+1} (0 at t = T-1)
@@ -147,7 +163,6 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         if (r < n) {
 #pragma unroll
           for (int a = 0; a < m; ++a) R0[W::KG + a * kG + r] = L.Kk[a][r];
-          R0[W::LAM + r] = lam_r;
         } else if (r == n) {
 #pragma unroll
           for (int a = 0; a < m; ++a) R0[W::KG + a * kG + n] = L.Kk[a][GroupLds<n, m>::W];
@@ -158,15 +173,10 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
       __syncthreads();
     }
   }
-  // ---------------- A + C (t up): gradx_t (grad_input, rocket.py:263-323 /
-  // cartpole.py:755-769) and the rollout y of the modified problem (linear,
-  // alpha = 1) in ONE pass: both walk t upward over the same (x_t, u_t) and share
-  // the Jacobian row and the step's two barriers — one latency-bound pass over T
-  // fewer than running them apart, the same arithmetic.
+  // per lane: row r of C and c_t[r] from registers in pass D
+  const bool crow_regs = c_offd == 0u && c_dif == 0u, cv_regs = cv_dif == 0u;
+  // ---------------- C (t up): the rollout y of the modified problem (linear, alpha = 1)
   {
-    float gx[p];
-#pragma unroll
-    for (int k = 0; k < p; ++k) gx[k] = 0.f;
     float yx = 0.f;                                        // lane r < n: y_t[r]
     for (int t = 0; t < T; ++t) {
       const size_t tb = (size_t)t * B + b;
@@ -178,15 +188,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         Kc[a] = r < n ? R0[W::KG + a * kG + r] : 0.f;
         kt[a] = R0[W::KG + a * kG + n];
       }
-      float Kq[m][n];                                     // K[t-1] of the reversed stack = K_{T-t}
-      if (t > 0) {
-        const float* Kp = K + ((size_t)(T - t) * B + b) * m * n;
-#pragma unroll
-        for (int a = 0; a < m; ++a)
-#pragma unroll
-          for (int l = 0; l < n; ++l) Kq[a][l] = Kp[a * n + l];
-      }
-      // C: y_t from y_t's state part (the previous step's D y)
+      // y_t from y_t's state part (the previous step's D y)
       float yr = r < n ? yx : 0.f;
 #pragma unroll
       for (int a = 0; a < m; ++a) {
@@ -195,73 +197,48 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         yr = (r == n + a) ? ya : yr;
       }
       if (valid && r < d) R0[W::Y + r] = yr;
-      const bool a_step = t > 0, c_step = t < T - 1;       // uniform
-      if (a_step || c_step) {
-        if (a_step && r < n) {
-#pragma unroll
-          for (int k = 0; k < p; ++k) I.gx[r][k] = gx[k];
-        }
-        if (c_step && r < d) I.vec[r] = yr;
+      if (t < T - 1) {                                     // uniform
+        if (r < d) I.vec[r] = yr;
         __syncthreads();
         if (r < n) {
           float Dr[d];
           md.template jac_row<false>(r, xt, ut, Dr);
-          if (a_step) {
-            float xx[n], ft[p];
-            D2::xx_row(r, theta, xt, ut, xx);
-            D2::xth_row(r, theta, xt, ut, ft);
-            float A[n];
+          float s = 0.f;
 #pragma unroll
-            for (int l = 0; l < n; ++l) {
-              float s = xx[l];
-#pragma unroll
-              for (int a = 0; a < m; ++a) s += Dr[n + a] * Kq[a][l];
-              A[l] = s;
-            }
-#pragma unroll
-            for (int k = 0; k < p; ++k) {
-              float s = 0.f;
-#pragma unroll
-              for (int l = 0; l < n; ++l) s += A[l] * I.gx[l][k];
-              gx[k] = ft[k] + s;
-            }
-          }
-          if (c_step) {
-            float s = 0.f;
-#pragma unroll
-            for (int j = 0; j < d; ++j) s += Dr[j] * I.vec[j];
-            yx = s;
-          }
+          for (int j = 0; j < d; ++j) s += Dr[j] * I.vec[j];
+          yx = s;
         }
         __syncthreads();
       }
-      if (valid && r < n) {
-#pragma unroll
-        for (int k = 0; k < p; ++k) R0[W::GX + k * kG + r] = gx[k];
-      }
     }
   }
-  // ---------------- D: w, dlam, dC, dc, dtheta
+  // ---------------- D: lam, w, dlam, dC, dc, dtheta (t down)
   {
-    float acc[p], gx1[p];
+    float acc[p];
 #pragma unroll
-    for (int k = 0; k < p; ++k) acc[k] = gx1[k] = 0.f;
-    if (r < kG) I.dlam[r] = 0.f;
+    for (int k = 0; k < p; ++k) acc[k] = 0.f;
+    float au[m];                                           // (D_u,t+1)^T mu_{t+1}
+#pragma unroll
+    for (int a = 0; a < m; ++a) au[a] = 0.f;
+    if (r < kG) { I.dlam[r] = 0.f; I.lam[r] = 0.f; }
     __syncthreads();
     for (int t = T - 1; t >= 0; --t) {
       const size_t tb = (size_t)t * B + b;
       const float* R0 = rec(t);
-      float xt[n], ut[m], y[d], Crow[d], gr = 0.f;
+      float xt[n], ut[m], y[d], Crow[d], cr = 0.f, gr = 0.f;
       load_tau(tb, xt, ut);
 #pragma unroll
       for (int j = 0; j < d; ++j) { y[j] = R0[W::Y + j]; Crow[j] = 0.f; }
       if (r < d) {
-        ld(Crow, C + (tb * d + r) * d);
+        if (crow_regs) {
+#pragma unroll
+          for (int j = 0; j < d; ++j) Crow[j] = j == r ? cdg : 0.f;
+        } else {
+          ld(Crow, C + (tb * d + r) * d);
+        }
+        cr = cv_regs ? cvr : c[tb * d + r];
         gr = r < n ? dl_dx[tb * n + r] : dl_du[tb * m + (r - n)];
       }
-      float gx[p];
-#pragma unroll
-      for (int k = 0; k < p; ++k) gx[k] = r < n ? R0[W::GX + k * kG + r] : 0.f;
       float tau[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) tau[i] = xt[i];
@@ -278,23 +255,23 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         st(dC + (tb * d + r) * d, dCr);
         dc[tb * d + r] = -yr;
       }
-      float dl1[n];
+      // row r of D_t -> LDS (t = T-1: only for the carry's D_u, F_{T-1} is zero)
+      if (r < n) {
+        float Fr[d];
+        md.template jac_row<false>(r, xt, ut, Fr);
 #pragma unroll
-      for (int i = 0; i < n; ++i) dl1[i] = I.dlam[i];      // dlam_{t+1}
-      float wr = gr, Dtd = 0.f;                            // w_t[r]; (D^T dlam_{t+1})[r]
+        for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
+      }
+      float wr = gr, Dtd = 0.f, Dtl = 0.f;                 // w_t[r]; (D^T dlam_{t+1})[r], (D^T lam_{t+1})[r]
+      float hx = 0.f;                                      // lane r < n: h_t[r] + (A_{t+1}^T mu_{t+1})[r]
       if (t < T - 1) {
-        float lam1[n];
-        const float* R1 = rec(t + 1);
-#pragma unroll
-        for (int i = 0; i < n; ++i) lam1[i] = R1[W::LAM + i];
         float Mc[d], Mp[p];
-        D2::mcol(r, theta, xt, ut, lam1, Mc);
-        D2::mp_row(r, theta, xt, ut, lam1, Mp);
-        if (r < n) {
-          float Fr[d];
-          md.template jac_row<false>(r, xt, ut, Fr);
+        {
+          float lam1[n];
 #pragma unroll
-          for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
+          for (int i = 0; i < n; ++i) lam1[i] = I.lam[i];  // lam_{t+1}
+          D2::mcol(r, theta, xt, ut, lam1, Mc);
+          D2::mp_row(r, theta, xt, ut, lam1, Mp);
         }
         __syncthreads();
         float z = 0.f;                                     // (M_t^T y_t)[r]
@@ -302,11 +279,11 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         for (int j = 0; j < d; ++j) z += Mc[j] * y[j];
         if (r < d) {
 #pragma unroll
-          for (int i = 0; i < n; ++i) Dtd += L.F[i][r] * dl1[i];
+          for (int i = 0; i < n; ++i) { Dtd += L.F[i][r] * I.dlam[i]; Dtl += L.F[i][r] * I.lam[i]; }
         }
         wr = gr - z;
-        // dtheta_t = -(y^T Mp) - (y^T (M_x + M_u Kq)) gradx_t - dlam_{t+1}^T gradx_{t+1}
-        //            + dlam_{t+1}^T (D_x + D_u Kq) gradx_t      (oracle/adjoint.py implicit_backward_fast)
+        // dtheta_t = -(y^T Mp) + h_t^T gradx_t - dlam_{t+1}^T gradx_{t+1},
+        // h_t = dlam_{t+1}^T (D_x + D_u Kq) - y^T (M_x + M_u Kq)   (oracle/adjoint.py implicit_backward_fast)
         float zu[m], du[m];
 #pragma unroll
         for (int a = 0; a < m; ++a) {
@@ -319,32 +296,58 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         }
         if (r < n) {
           const float* Kp = K + ((size_t)(T - 1 - t) * B + b) * m * n;   // K[t] of the reversed stack
-          float sx = z, s2 = Dtd;
+          float sx = z, s2 = Dtd, cu = 0.f;
 #pragma unroll
           for (int a = 0; a < m; ++a) {
             const float Kal = Kp[a * n + r];
             sx += zu[a] * Kal;
             s2 += du[a] * Kal;
+            cu += au[a] * Kal;
           }
-          const float hx = s2 - sx, dlr = I.dlam[r];
+          // the carry A_{t+1}^T mu_{t+1}: column r of the rows step t+1 left in LDS,
+          // plus Krev^T (D_u,t+1)^T mu_{t+1} (A_{t+1} pairs D_{t+1} with this step's Kq)
+          float cx = 0.f;
 #pragma unroll
-          for (int k = 0; k < p; ++k) acc[k] += hx * gx[k] - dlr * gx1[k];
+          for (int i = 0; i < n; ++i) cx += I.ax[i][r];
+          hx = (s2 - sx) + (cx + cu);
         }
       }
       // dlam_t = Cxx y_x + Cxu y_u - w_x + F_x^T dlam_{t+1}   (lqr_step_explicit.py:321-335)
-      float nd = 0.f;
+      // lam_t  = Cxx x + Cxu u + c_x + F_x^T lam_{t+1}        (pass B's recursion, 305-319)
+      float nd = 0.f, nl = 0.f;
       if (r < n) {
-        float s = 0.f, s2 = 0.f;
+        float s = 0.f, s2 = 0.f, q = 0.f, q2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < n; ++j) s += Crow[j] * y[j];
+        for (int j = 0; j < n; ++j) { s += Crow[j] * y[j]; q += Crow[j] * xt[j]; }
 #pragma unroll
-        for (int a = 0; a < m; ++a) s2 += Crow[n + a] * y[n + a];
+        for (int a = 0; a < m; ++a) { s2 += Crow[n + a] * y[n + a]; q2 += Crow[n + a] * ut[a]; }
         nd = ((s + s2) - wr) + Dtd;
+        nl = ((q + q2) + cr) + Dtl;
       }
+      // mu_t = h_t - dlam_t (+ the carry); dtheta += f_theta,t^T mu_t; this
+      // step's carry rows for step t-1: mu_t[i] * x_grad_xtm1[i][:], (D_u,t)^T mu_t
+      float mu = 0.f;
+      if (t >= 1) {                                        // uniform
+        float axr[n];
+        if (r < n) {
+          mu = hx - nd;
+          float ft[p];
+          D2::xth_row(r, theta, xt, ut, ft);
 #pragma unroll
-      for (int k = 0; k < p; ++k) gx1[k] = gx[k];
-      __syncthreads();
-      if (r < n) I.dlam[r] = nd;
+          for (int k = 0; k < p; ++k) acc[k] += ft[k] * mu;
+          D2::xx_row(r, theta, xt, ut, axr);
+        }
+#pragma unroll
+        for (int a = 0; a < m; ++a) au[a] = group_sum(r < n ? L.F[r][n + a] * mu : 0.f);
+        __syncthreads();                                   // every lane is done with dlam, lam, ax of t+1
+        if (r < n) {
+#pragma unroll
+          for (int l = 0; l < n; ++l) I.ax[r][l] = axr[l] * mu;
+        }
+      } else {
+        __syncthreads();
+      }
+      if (r < n) { I.dlam[r] = nd; I.lam[r] = nl; }
       __syncthreads();
     }
     float dth = 0.f;

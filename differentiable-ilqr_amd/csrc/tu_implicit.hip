@@ -13,17 +13,52 @@ namespace dilqr {
 // (the Lagrangian Hessian of the dynamics), after which dC, dc, dtheta are the
 // KKT gradients of the adjoint solve with r = w, whose trajectory is that same
 // solve's y.  Per problem (one lane), three passes over T:
-//   B (t down)   : primal costates lam_t -> ws; M_t; Riccati step with C_t + M_t^T,
-//                  c_back = -g_t, active set masked (u_zero_I engine) -> ws
-//   A+C (t up)   : gradx_t (grad_input's closed-loop d x_t / d theta, with the
-//                  reference's reversed-K and x_grad_xtm1 quirks) and the rollout
-//                  y (no line search) -> ws, one Jacobian per step for both
-//   D (t down)   : w_t = g_t - M_t^T y_t, dlam; dC_t, dc_t out; dtheta accumulated.
+//   B (t down): primal costates lam_t (registers); M_t; Riccati step with
+//               C_t + M_t^T, c_back = -g_t, active set masked (u_zero_I engine);
+//               the gains (K_t, k_t) -> ws
+//   C (t up)  : the rollout y of the modified problem (linear, alpha = 1) -> ws
+//   D (t down): lam_t again (the same recursion as B: nothing stored), w_t =
+//               g_t - M_t^T y_t, dlam; dC_t, dc_t out; dtheta.
+// dtheta = sum_t [-y_t^T Mp_t + h_t^T gradx_t] where gradx_t is grad_input's
+// closed-loop d x_t / d theta (cartpole.py:755-769: gradx_t = f_theta,t +
+// A_t gradx_{t-1}, A_t = D_x,t + D_u,t Krev_t, with the reference's reversed-K
+// and x_grad_xtm1 quirks).  Rather than roll gradx up (n*p floats per step
+// stored and re-read), pass D carries its adjoint mu_t = h_t + A_{t+1}^T
+// mu_{t+1} down and adds f_theta,t^T mu_t: the same sum, O(n) state, no
+// storage.  The workspace is two component-major records per (t, b), the
+// gains and y (SoaRec planes: a wave's loads are 1-KiB runs); the caller's
+// tensors are the only other traffic.
 template <class Model> struct ImplicitWs {
-  static constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m;
-  static constexpr int GX = 0, LAM = n * p, KG = LAM + n, Y = KG + m * n + m;
-  static constexpr int REC = ((Y + d) + 3) / 4 * 4;
+  static constexpr int n = Model::N, m = Model::M, d = n + m;
+  static constexpr int G = m * n + m;                  // K_t, k_t of the modified Riccati step
+  // floats per (t, b): the gain planes, the y planes, slack so the y region
+  // starts 16-byte aligned whatever T*B is
+  static constexpr int REC = G + d + 4;
+  static DEV size_t y_off(int T, int B) { return ((size_t)T * B * G + 3) / 4 * 4; }
 };
+
+// lam_t = Cxx x + Cxu u + c_x + F_x^T lam_{t+1}   (lqr_step_explicit.py:305-319);
+// D is zero at t = T-1.  Passes B and D run this same function on the same
+// inputs, so they hold the same bits.
+template <int n, int m>
+DEV void costate_step(const float (&Ct)[n + m][n + m], const float (&cx)[n], const float (&xt)[n],
+                      const float (&ut)[m], const float (&D)[n][n + m], float (&lam)[n]) {
+  float nl[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    float s = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < n; ++j) s += Ct[i][j] * xt[j];
+#pragma unroll
+    for (int a = 0; a < m; ++a) s2 += Ct[i][n + a] * ut[a];
+    float s3 = 0.f;
+#pragma unroll
+    for (int l = 0; l < n; ++l) s3 += D[l][i] * lam[l];
+    nl[i] = ((s + s2) + cx[i]) + s3;
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i) lam[i] = nl[i];
+}
 
 template <class Model>
 __global__ void __launch_bounds__(kBlock) k_implicit_backward(
@@ -33,22 +68,29 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     float* __restrict__ dC, float* __restrict__ dc, float* __restrict__ dtheta) {
   using D2 = typename D2Of<Model>::type;
   using W = ImplicitWs<Model>;
-  constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m, R = W::REC;
+  constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m, G = W::G;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   Model md; md.load(theta);
-  auto rec = [&](int t) { return ws + ((size_t)t * B + b) * R; };
+  float* const wsG = ws;
+  float* const wsY = ws + W::y_off(T, B);
   auto active = [&](size_t tb, int a, float ua) -> bool {
     if (bd.mode == DILQR_BOUNDS_NONE) return false;
     return fabsf(ua - bound_lo(bd, tb * m + a)) <= 1e-8f || fabsf(ua - bound_hi(bd, tb * m + a)) <= 1e-8f;
   };
+  auto zero_D = [](float (&D)[n][d]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+#pragma unroll
+      for (int j = 0; j < d; ++j) D[i][j] = 0.f;
+  };
   // Pass B also tests whether the problem's C_t are one diagonal matrix for all
   // t (every off-diagonal word +0.0, the diagonals equal to step T-1's bit for
-  // bit — the reference's callers pass diag(q) repeated over t): pass D then
-  // takes C_t from those registers instead of reading it again (the same
-  // values, so the same arithmetic; 144 B per step and problem not re-read).
-  float cdiag[d];
-  unsigned c_offd = 0u, c_dif = 0u;
+  // bit — the reference's callers pass diag(q) repeated over t) and whether the
+  // c_t are one vector: pass D then takes them from these registers instead of
+  // reading them again (the same values, so the same arithmetic).
+  float cdiag[d], cvec[d];
+  unsigned c_offd = 0u, c_dif = 0u, cv_dif = 0u;
   // ---------------- B: costates, M_t, Riccati of the C + M^T problem
   {
     RiccatiState<n, m> rs;
@@ -63,11 +105,12 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       ld(gxx, dl_dx + tb * n); ld(gu, dl_du + tb * m);
       if (t == T - 1) {
 #pragma unroll
-        for (int i = 0; i < d; ++i) cdiag[i] = Ct[i][i];
+        for (int i = 0; i < d; ++i) { cdiag[i] = Ct[i][i]; cvec[i] = ct[i]; }
       }
 #pragma unroll
       for (int i = 0; i < d; ++i) {
         c_dif |= __float_as_uint(Ct[i][i]) ^ __float_as_uint(cdiag[i]);
+        cv_dif |= __float_as_uint(ct[i]) ^ __float_as_uint(cvec[i]);
 #pragma unroll
         for (int j = 0; j < d; ++j)
           if (j != i) c_offd |= __float_as_uint(Ct[i][j]);
@@ -78,10 +121,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         md.jacobian(xt, ut, D);
         D2::lag_hess(theta, xt, ut, lam, Mt);             // lam = lam_{t+1}
       } else {
-#pragma unroll
-        for (int i = 0; i < n; ++i)
-#pragma unroll
-          for (int j = 0; j < d; ++j) D[i][j] = 0.f;
+        zero_D(D);
 #pragma unroll
         for (int i = 0; i < d; ++i)
 #pragma unroll
@@ -102,84 +142,32 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       float Kt[m][n], kt[m];
       if (bd.mode != DILQR_BOUNDS_NONE) rs.template step<GAIN_ZERO_I>(Cp, cb, D, zI, lb, ub, Kt, kt);
       else rs.template step<GAIN_UNC>(Cp, cb, D, zI, lb, ub, Kt, kt);
-      float* r = rec(t);
-      st2(r + W::KG, Kt);
+      float gr[G];
 #pragma unroll
-      for (int a = 0; a < m; ++a) r[W::KG + m * n + a] = kt[a];
-      // lam_t = Cxx x + Cxu u + c_x + F_x^T lam_{t+1}   (lqr_step_explicit.py:305-319)
-      float nl[n];
+      for (int a = 0; a < m; ++a) {
 #pragma unroll
-      for (int i = 0; i < n; ++i) {
-        float s = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int j = 0; j < n; ++j) s += Ct[i][j] * xt[j];
-#pragma unroll
-        for (int a = 0; a < m; ++a) s2 += Ct[i][n + a] * ut[a];
-        float s3 = 0.f;
-#pragma unroll
-        for (int l = 0; l < n; ++l) s3 += D[l][i] * lam[l];
-        nl[i] = ((s + s2) + ct[i]) + s3;
+        for (int j = 0; j < n; ++j) gr[a * n + j] = Kt[a][j];
+        gr[m * n + a] = kt[a];
       }
+      SoaRec<G>::store(wsG, gr, T, t, B, b);
+      float cx[n];
 #pragma unroll
-      for (int i = 0; i < n; ++i) { lam[i] = nl[i]; r[W::LAM + i] = nl[i]; }
+      for (int i = 0; i < n; ++i) cx[i] = ct[i];
+      costate_step<n, m>(Ct, cx, xt, ut, D, lam);
     }
   }
-  // ---------------- A + C (t up): gradx_t (grad_input's closed-loop d x_t /
-  // d theta, cartpole.py:755-769) and the rollout y of the modified problem
-  // (linear, alpha = 1) in ONE pass: both walk t upward over the same (x_t, u_t)
-  // and share the Jacobian D_t — one latency-bound pass over T fewer than
-  // running them apart, the same arithmetic.
+  const bool c_regs = c_offd == 0u && c_dif == 0u, cv_regs = cv_dif == 0u;
+  // ---------------- C (t up): the rollout y of the modified problem (linear,
+  // alpha = 1, active controls zeroed)
   {
-    float gx[n][p], yx[n];
+    float yx[n];
 #pragma unroll
-    for (int i = 0; i < n; ++i) {
-      yx[i] = 0.f;
-#pragma unroll
-      for (int k = 0; k < p; ++k) gx[i][k] = 0.f;
-    }
-    st2(rec(0) + W::GX, gx);
+    for (int i = 0; i < n; ++i) yx[i] = 0.f;
     for (int t = 0; t < T; ++t) {
       size_t tb = (size_t)t * B + b;
-      float* r = rec(t);
-      float xt[n], ut[m], Kt[m][n], kt[m];
+      float xt[n], ut[m], gr[G];
       ld(xt, x + tb * n); ld(ut, u + tb * m);
-      ld2(Kt, r + W::KG);
-#pragma unroll
-      for (int a = 0; a < m; ++a) kt[a] = r[W::KG + m * n + a];
-      float Kq[m][n];
-      if (t >= 1) ld2(Kq, K + ((size_t)(T - t) * B + b) * m * n);   // K[t-1] of the reversed stack = K_{T-t}
-      float D[n][d];
-      md.jacobian(xt, ut, D);
-      if (t >= 1) {
-        float ft[n][p];
-        D2::f_theta(theta, xt, ut, ft);
-        float A[n][n];
-#pragma unroll
-        for (int i = 0; i < n; ++i)
-#pragma unroll
-          for (int l = 0; l < n; ++l) {
-            float s_ = D[i][l];
-            if (D2Of<Model>::XX00_ZERO && i == 0 && l == 0) s_ = 0.f;
-#pragma unroll
-            for (int a = 0; a < m; ++a) s_ += D[i][n + a] * Kq[a][l];
-            A[i][l] = s_;
-          }
-        float ng[n][p];
-#pragma unroll
-        for (int i = 0; i < n; ++i)
-#pragma unroll
-          for (int k = 0; k < p; ++k) {
-            float s_ = 0.f;
-#pragma unroll
-            for (int l = 0; l < n; ++l) s_ += A[i][l] * gx[l][k];
-            ng[i][k] = ft[i][k] + s_;
-          }
-#pragma unroll
-        for (int i = 0; i < n; ++i)
-#pragma unroll
-          for (int k = 0; k < p; ++k) gx[i][k] = ng[i][k];
-        st2(r + W::GX, gx);
-      }
+      SoaRec<G>::load(gr, wsG, T, t, B, b);
       float y[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) y[i] = yx[i];
@@ -187,12 +175,13 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       for (int a = 0; a < m; ++a) {
         float s_ = 0.f;
 #pragma unroll
-        for (int j = 0; j < n; ++j) s_ += Kt[a][j] * yx[j];
-        y[n + a] = active(tb, a, ut[a]) ? 0.f : (s_ + 0.f) + kt[a];
+        for (int j = 0; j < n; ++j) s_ += gr[a * n + j] * yx[j];
+        y[n + a] = active(tb, a, ut[a]) ? 0.f : (s_ + 0.f) + gr[m * n + a];
       }
-#pragma unroll
-      for (int i = 0; i < d; ++i) r[W::Y + i] = y[i];
+      SoaRec<d>::store(wsY, y, T, t, B, b);
       if (t < T - 1) {
+        float D[n][d];
+        md.jacobian(xt, ut, D);
 #pragma unroll
         for (int i = 0; i < n; ++i) {
           float s_ = 0.f;
@@ -203,22 +192,19 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       }
     }
   }
-  // ---------------- D: w, dlam, dC, dc, dtheta
+  // ---------------- D: lam, w, dlam, dC, dc, dtheta (t down)
   {
-    float dlam[n], gx1[n][p], dth[p];
+    float lam[n], dlam[n], mu[n], ax[n], au[m], dth[p];
 #pragma unroll
-    for (int i = 0; i < n; ++i) {
-      dlam[i] = 0.f;
+    for (int i = 0; i < n; ++i) { lam[i] = 0.f; dlam[i] = 0.f; mu[i] = 0.f; ax[i] = 0.f; }
 #pragma unroll
-      for (int k = 0; k < p; ++k) gx1[i][k] = 0.f;
-    }
+    for (int a = 0; a < m; ++a) au[a] = 0.f;
 #pragma unroll
     for (int k = 0; k < p; ++k) dth[k] = 0.f;
     for (int t = T - 1; t >= 0; --t) {
       size_t tb = (size_t)t * B + b;
-      float* r = rec(t);
-      float Ct[d][d], xt[n], ut[m], gxx[n], gu[m], y[d], gx[n][p];
-      if (c_offd == 0u && c_dif == 0u) {
+      float Ct[d][d], ct[d], xt[n], ut[m], gxx[n], gu[m], y[d];
+      if (c_regs) {
 #pragma unroll
         for (int i = 0; i < d; ++i)
 #pragma unroll
@@ -226,11 +212,15 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       } else {
         ld2(Ct, C + tb * d * d);
       }
+      if (cv_regs) {
+#pragma unroll
+        for (int i = 0; i < d; ++i) ct[i] = cvec[i];
+      } else {
+        ld(ct, c + tb * d);
+      }
       ld(xt, x + tb * n); ld(ut, u + tb * m);
       ld(gxx, dl_dx + tb * n); ld(gu, dl_du + tb * m);
-#pragma unroll
-      for (int i = 0; i < d; ++i) y[i] = r[W::Y + i];
-      ld2(gx, r + W::GX);
+      SoaRec<d>::load(y, wsY, T, t, B, b);
       float tau[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) tau[i] = xt[i];
@@ -246,16 +236,15 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       }
       st2(dC + tb * d * d, dCt);
       st(dc + tb * d, dct);
-      float wx[n];
-      float D[n][d];
+      float D[n][d], wx[n], hx[n];
+      md.jacobian(xt, ut, D);             // D_t (t = T-1: only for A_{T-1} of the mu carry)
+      // the carry A_{t+1}^T mu_{t+1} = (D_x,t+1)^T mu_{t+1} + Krev^T (D_u,t+1)^T mu_{t+1},
+      // Krev = K[t] of the reversed stack = K_{T-1-t}: the gain grad_input pairs with step t+1
       if (t < T - 1) {
-        float lam1[n], Mt[d][d], Mp[d][p], Kq[m][n];
-#pragma unroll
-        for (int i = 0; i < n; ++i) lam1[i] = rec(t + 1)[W::LAM + i];
-        md.jacobian(xt, ut, D);
-        D2::lag_hess(theta, xt, ut, lam1, Mt);
-        D2::lag_dparam(theta, xt, ut, lam1, Mp);
-        ld2(Kq, K + ((size_t)(T - 1 - t) * B + b) * m * n);   // K[t] of the reversed stack
+        float Kq[m][n], Mt[d][d], Mp[d][p];
+        ld2(Kq, K + ((size_t)(T - 1 - t) * B + b) * m * n);
+        D2::lag_hess(theta, xt, ut, lam, Mt);          // lam = lam_{t+1}
+        D2::lag_dparam(theta, xt, ut, lam, Mp);
         // w_t = g_t - M_t^T y_t
 #pragma unroll
         for (int k = 0; k < n; ++k) {
@@ -264,15 +253,14 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
           for (int j = 0; j < d; ++j) s += Mt[j][k] * y[j];
           wx[k] = gxx[k] - s;
         }
-        // dtheta_t = -(y^T Mp) - (y^T (M_x + M_u Kq)) gradx_t - dlam_{t+1}^T gradx_{t+1}
-        //            + dlam_{t+1}^T (D_x + D_u Kq) gradx_t
-        float hx[n], hp[p];
+        // dtheta_t = -(y^T Mp) + h_t^T gradx_t - dlam_{t+1}^T gradx_{t+1} with
+        // h_t = dlam_{t+1}^T (D_x + D_u Kq) - y^T (M_x + M_u Kq)
 #pragma unroll
         for (int k = 0; k < p; ++k) {
           float s = 0.f;
 #pragma unroll
           for (int j = 0; j < d; ++j) s += y[j] * Mp[j][k];
-          hp[k] = s;
+          dth[k] -= s;
         }
 #pragma unroll
         for (int l = 0; l < n; ++l) {
@@ -293,39 +281,78 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
           }
           hx[l] = s2 - s;
         }
+        // mu carry from step t+1 (A_{t+1} pairs D_{t+1} with this step's Kq)
 #pragma unroll
-        for (int k = 0; k < p; ++k) {
-          float s = -hp[k];
+        for (int l = 0; l < n; ++l) {
+          float s = ax[l];
 #pragma unroll
-          for (int l = 0; l < n; ++l) s += hx[l] * gx[l][k] - dlam[l] * gx1[l][k];
-          dth[k] += s;
+          for (int a = 0; a < m; ++a) s += Kq[a][l] * au[a];
+          hx[l] += s;
         }
       } else {
 #pragma unroll
-        for (int k = 0; k < n; ++k) wx[k] = gxx[k];
-#pragma unroll
-        for (int i = 0; i < n; ++i)
-#pragma unroll
-          for (int j = 0; j < d; ++j) D[i][j] = 0.f;
+        for (int k = 0; k < n; ++k) { wx[k] = gxx[k]; hx[k] = 0.f; }
       }
-      // dlam_t = Cxx y_x + Cxu y_u - w_x + F_x^T dlam_{t+1}   (lqr_step_explicit.py:321-335)
-      float nd[n];
+      // dlam_t = Cxx y_x + Cxu y_u - w_x + F_x^T dlam_{t+1}   (lqr_step_explicit.py:321-335);
+      // lam_t by the pass-B recursion (F_t = D_t for t < T-1, zero at T-1)
+      float cx[n];
 #pragma unroll
-      for (int i = 0; i < n; ++i) {
-        float s = 0.f, s2 = 0.f, s3 = 0.f;
+      for (int i = 0; i < n; ++i) cx[i] = ct[i];
+      {
+        float Dl[n][d];
+        if (t < T - 1) {
 #pragma unroll
-        for (int j = 0; j < n; ++j) s += Ct[i][j] * y[j];
+          for (int i = 0; i < n; ++i)
 #pragma unroll
-        for (int a = 0; a < m; ++a) s2 += Ct[i][n + a] * y[n + a];
+            for (int j = 0; j < d; ++j) Dl[i][j] = D[i][j];
+        } else {
+          zero_D(Dl);
+        }
+        float nd[n];
 #pragma unroll
-        for (int l = 0; l < n; ++l) s3 += D[l][i] * dlam[l];
-        nd[i] = ((s + s2) - wx[i]) + s3;
+        for (int i = 0; i < n; ++i) {
+          float s = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+          for (int j = 0; j < n; ++j) s += Ct[i][j] * y[j];
+#pragma unroll
+          for (int a = 0; a < m; ++a) s2 += Ct[i][n + a] * y[n + a];
+#pragma unroll
+          for (int l = 0; l < n; ++l) s3 += Dl[l][i] * dlam[l];
+          nd[i] = ((s + s2) - wx[i]) + s3;
+        }
+#pragma unroll
+        for (int i = 0; i < n; ++i) dlam[i] = nd[i];
+        costate_step<n, m>(Ct, cx, xt, ut, Dl, lam);
       }
+      if (t >= 1) {
+        // mu_t = h_t - dlam_t (+ the carry, folded into h_t above); dtheta += f_theta,t^T mu_t
 #pragma unroll
-      for (int i = 0; i < n; ++i) {
-        dlam[i] = nd[i];
+        for (int l = 0; l < n; ++l) mu[l] = hx[l] - dlam[l];
+        float ft[n][p];
+        D2::f_theta(theta, xt, ut, ft);
 #pragma unroll
-        for (int k = 0; k < p; ++k) gx1[i][k] = gx[i][k];
+        for (int k = 0; k < p; ++k) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < n; ++i) s += ft[i][k] * mu[i];
+          dth[k] += s;
+        }
+        // the next step's carry: (D_x,t)^T mu_t (the x_grad_xtm1 quirk: no D[0][0]) and (D_u,t)^T mu_t
+#pragma unroll
+        for (int l = 0; l < n; ++l) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < n; ++i)
+            if (!(D2Of<Model>::XX00_ZERO && i == 0 && l == 0)) s += D[i][l] * mu[i];
+          ax[l] = s;
+        }
+#pragma unroll
+        for (int a = 0; a < m; ++a) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < n; ++i) s += D[i][n + a] * mu[i];
+          au[a] = s;
+        }
       }
     }
     st(dtheta + (size_t)b * p, dth);
@@ -361,7 +388,7 @@ int dilqr_implicit_backward_f32(int model, int T, int B, const float* theta, con
   if (model == DILQR_MODEL_ROCKET)
     return launch_implicit_rocket(ImplicitArgs{T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta,
                                                S(stream)});
-  MODEL_SWITCH_TPP(model, (k_implicit_backward<MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
+  MODEL_SWITCH_TPP_D2(model, (k_implicit_backward<MD><<<grid_for(B), kBlock, 0, S(stream)>>>(
                           T, B, theta, C, c, x, u, K, dl_dx, dl_du, bd, ws, dC, dc, dtheta)));
   return launched();
 }
