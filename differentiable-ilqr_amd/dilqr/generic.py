@@ -212,11 +212,13 @@ def approximate_cost(x, u, cost, diff):
 
 # ---------------------------------------------------------------- one LQR step (forward)
 def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u_lower, u_upper, delta_u,
-                     decay, max_ls, u_zero_I=None):
+                     decay, max_ls, u_zero_I=None, extras=False):
     """LQRStepFn.forward of the DiLQR step (lqr_step_explicit.py:625-650): the
     HIP Riccati sweep in delta space (c_back = C tau + c fused), then the line
     search of lqr_forward (166-263) with the true dynamics/cost.  Returns
-    (new_x, new_u, costs [B], full_du_norm [B])."""
+    (new_x, new_u, costs [B], full_du_norm [B]); with extras also the final
+    step sizes [B] (one decay undone where the last pass still failed,
+    254-255) and the sweep's pnqp iteration count."""
     B = x.shape[1]
     lo = u_lower if (u_lower is None or isinstance(u_lower, float)) else u_lower.detach().contiguous()
     hi = u_upper if (u_upper is None or isinstance(u_upper, float)) else u_upper.detach().contiguous()
@@ -230,10 +232,11 @@ def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u
         # lqr_step_explicit.py:132-135: the sweep's relative box clipped to
         # +-delta_u (exact values), c_back formed here
         rlo, rhi = ops.delta_u_sweep_bounds(lo, hi, ud, delta_u)
-        K, k, _ = ops.lqr_backward(Cd, ops.c_back(Cd, cd, xd, ud), Fd, n, m, u_lower=rlo, u_upper=rhi)
+        K, k, nqp = ops.lqr_backward(Cd, ops.c_back(Cd, cd, xd, ud), Fd, n, m, u_lower=rlo, u_upper=rhi,
+                                     want_nqp=extras)
     else:
-        K, k, _ = ops.lqr_backward(Cd, cd, Fd, n, m, x=xd, u=ud, u_lower=lo, u_upper=hi,
-                                   u_zero_I=zI if lo is None else None)
+        K, k, nqp = ops.lqr_backward(Cd, cd, Fd, n, m, x=xd, u=ud, u_lower=lo, u_upper=hi,
+                                     u_zero_I=zI if lo is None else None, want_nqp=extras and lo is not None)
     old_cost = traj_cost(T, x, u, true_cost)
     alphas = torch.ones(B, device=x.device)
     cur_cost, full_du_norm = None, None
@@ -277,6 +280,11 @@ def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u
                 full_du_norm = (u - new_u).transpose(1, 2).contiguous().view(B, -1).norm(2, 1)
             alphas = torch.where(cur_cost > old_cost, alphas * decay, alphas)
             i += 1
+        if extras:
+            alphas = torch.where(cur_cost > old_cost, alphas / decay, alphas)
+    if extras:
+        n_qp = int(nqp.max().item()) if nqp is not None else 0
+        return new_x, new_u, cur_cost, full_du_norm, alphas, n_qp
     return new_x, new_u, cur_cost, full_du_norm
 
 

@@ -9,7 +9,7 @@ import torch
 from torch.autograd import Function
 
 from . import _native as N
-from . import ops
+from . import generic, ops
 from .definitions import QuadCost
 
 
@@ -32,9 +32,15 @@ def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta
             if no_op_forward:                                   # lqr_step.py:277-282
                 ctx.save_for_backward(x_init, C, c, F, f, x, u)
                 return x.clone(), u.clone()
-            if not isinstance(true_cost, QuadCost):
-                raise NotImplementedError("dilqr: true_cost must be a QuadCost on the HIP path")
-            m_id = ops.model_id_of(true_dynamics)
+            m_id = ops.generic_model_id(true_dynamics)
+            if not isinstance(true_cost, QuadCost) or m_id is None:
+                # a generic true_cost / true_dynamics (lqr_step.py:224-234): the HIP
+                # sweep, the rollout with the user's Modules in torch
+                nx, nu, costs, full_du_norm, alphas, n_qp = generic.lqr_step_forward(
+                    T, n_state, n_ctrl, x_init, C, c, F, x, u, true_cost, true_dynamics, lo, hi, delta_u,
+                    linesearch_decay, max_linesearch_iter, u_zero_I=zI, extras=True)
+                ctx.save_for_backward(x_init, C, c, F, f, nx, nu)
+                return nx, nu, torch.tensor([float(n_qp)]), costs, full_du_norm, alphas.mean()
             if delta_u is not None:                             # lqr_step.py:130-135
                 rlo, rhi = ops.delta_u_sweep_bounds(lo, hi, u, delta_u)
                 K, k, nqp = ops.lqr_backward(C, ops.c_back(C.detach(), c.detach(), x, u), F, n_state, n_ctrl,

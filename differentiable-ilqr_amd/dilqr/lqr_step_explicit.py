@@ -17,7 +17,7 @@ import torch
 from torch.autograd import Function
 
 from . import _native as N
-from . import ops
+from . import generic, ops
 from .definitions import LinDx, QuadCost
 
 
@@ -54,14 +54,20 @@ def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta
         def forward(ctx, x_init, C, c, F, f=None, theta=None, if_converge=False):
             assert current_x is not None and current_u is not None
             x, u = current_x.detach(), current_u.detach()
-            m_id = ops.model_id_of(true_dynamics)
+            m_id = ops.generic_model_id(true_dynamics)
             if no_op_forward:
                 K, _, _ = sweep(C, c, F, x, u)
                 ctx.save_for_backward(x_init, C, c, F, f, x, u, theta, K)
                 ctx.model = true_dynamics
                 return x.clone(), u.clone()
-            if not isinstance(true_cost, QuadCost):
-                raise NotImplementedError("dilqr: true_cost must be a QuadCost on the HIP path")
+            if not isinstance(true_cost, QuadCost) or m_id is None:
+                # a generic true_cost / true_dynamics (lqr_step_explicit.py:226-236):
+                # the HIP sweep, the rollout with the user's Modules in torch
+                nx, nu, costs, full_du_norm, alphas, n_qp = generic.lqr_step_forward(
+                    T, n_state, n_ctrl, x_init, C, c, F, x, u, true_cost, true_dynamics, lo, hi, delta_u,
+                    linesearch_decay, max_linesearch_iter, u_zero_I=zI, extras=True)
+                ctx.save_for_backward(x_init, C, c, F, f, nx, nu)
+                return nx, nu, torch.tensor([float(n_qp)]), costs, full_du_norm, alphas.mean()
             K, k, nqp = sweep(C, c, F, x, u, want_nqp=lo is not None)
             if m_id == N.MODEL_LINDX:
                 th, Fd, fd = None, true_dynamics.F, true_dynamics.f

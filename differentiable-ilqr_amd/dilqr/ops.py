@@ -27,6 +27,15 @@ def model_id_of(dx):
     return mid
 
 
+def generic_model_id(dx):
+    """model_id_of, or None for a dynamics Module the HIP kernels do not model
+    (the caller then runs it in torch)."""
+    from .definitions import LinDx
+    if isinstance(dx, LinDx):
+        return N.MODEL_LINDX
+    return getattr(dx, "model_id", None)
+
+
 def theta_of(dx, like):
     return dx._theta(like)
 

@@ -718,6 +718,67 @@ def case_api():
 
 
 # --------------------------------------------------------------------------
+# M. LQRStep (both variants) with a generic true_cost / true_dynamics: the line
+#    search evaluates true_cost(new_xut) and true_dynamics(x, u)
+#    (lqr_step_explicit.py:226-236, lqr_step.py:224-234)
+# --------------------------------------------------------------------------
+def case_stepgen():
+    import dynamics as ref_dyn
+    print("M. LQRStep with generic true_cost / true_dynamics")
+    dt = torch.float64
+    out = {}
+    with default_dtype(dt), contextlib.redirect_stdout(io.StringIO()):
+        # ---- pendulum, non-quadratic true_cost, the sweep on the true objective's C, c
+        T, B = 10, 8
+        rng = np.random.RandomState(31)
+        dxp = model("pendulum")
+        x0 = xinit_for("pendulum", B, rng)
+        u = rng.uniform(-1, 1, (T, B, 1))
+        wq = 0.3 * rng.normal(size=4)
+        X0, U = torch.tensor(x0), torch.tensor(u)
+        Q, P = true_cost(dxp, T, B, dt)
+        cost = NQCost(torch.tensor(wq))
+        with torch.no_grad():
+            X = R.util.get_traj(T, U, x_init=X0, dynamics=dxp)
+            F, f = R.mpc_explicit.MPC(3, 1, T, lqr_iter=1).linearize_dynamics(X, U, dxp, diff=False)
+        out.update(nq_x0=x0, nq_u=u, nq_w=wq, nq_X=np_(X), nq_F=np_(F), nq_f=np_(f))
+        for tag, mod in (("explicit", R.lqr_step_explicit), ("classic", R.lqr_step)):
+            step = mod.LQRStep(3, 1, T, u_lower=-2.0, u_upper=2.0, true_cost=cost, true_dynamics=dxp,
+                               current_x=X, current_u=U, linesearch_decay=0.2, max_linesearch_iter=5)
+            args = (X0, Q, P, F, f) + ((None,) if tag == "explicit" else ())
+            with torch.no_grad():
+                nx, nu, nqp, costs, du, malpha = step(*args)
+            out.update({f"nq_{tag}_nx": np_(nx), f"nq_{tag}_nu": np_(nu), f"nq_{tag}_costs": np_(costs),
+                        f"nq_{tag}_du": np_(du), f"nq_{tag}_malpha": np_(malpha), f"nq_{tag}_nqp": np_(nqp)})
+        # ---- NNDynamics true_dynamics (n=5, m=1), quadratic true_cost, AUTO_DIFF linearisation
+        torch.manual_seed(5)
+        nn_dx = ref_dyn.NNDynamics(5, 1, hidden_sizes=[32], activation="sigmoid")
+        for i, fc in enumerate(nn_dx.fcs):
+            out[f"nn_W{i}"], out[f"nn_b{i}"] = np_(fc.weight), np_(fc.bias)
+        x0 = 0.3 * rng.normal(size=(B, 5))
+        u = 0.3 * rng.normal(size=(T, B, 1))
+        L = rng.normal(size=(T, B, 6, 6)) * 0.3
+        C = L @ np.swapaxes(L, -1, -2) + np.eye(6)
+        c = 0.1 * rng.normal(size=(T, B, 6))
+        X0, U, Ct, ct = (torch.tensor(a) for a in (x0, u, C, c))
+        X = R.util.get_traj(T, U, x_init=X0, dynamics=nn_dx).detach()
+        F, f = R.mpc_explicit.MPC(5, 1, T, lqr_iter=1, grad_method=R.mpc_explicit.GradMethods.AUTO_DIFF
+                                  ).linearize_dynamics(X, U, nn_dx, diff=False)
+        F, f = F.detach(), f.detach()
+        out.update(nn_x0=x0, nn_u=u, nn_C=C, nn_c=c, nn_X=np_(X), nn_F=np_(F), nn_f=np_(f))
+        for tag, mod in (("explicit", R.lqr_step_explicit), ("classic", R.lqr_step)):
+            step = mod.LQRStep(5, 1, T, u_lower=-1.0, u_upper=1.0, true_cost=R.mpc_explicit.QuadCost(Ct, ct),
+                               true_dynamics=nn_dx, current_x=X, current_u=U, linesearch_decay=0.2,
+                               max_linesearch_iter=10)
+            args = (X0, Ct, ct, F, f) + ((None,) if tag == "explicit" else ())
+            with torch.no_grad():
+                nx, nu, nqp, costs, du, malpha = step(*args)
+            out.update({f"nn_{tag}_nx": np_(nx), f"nn_{tag}_nu": np_(nu), f"nn_{tag}_costs": np_(costs),
+                        f"nn_{tag}_du": np_(du), f"nn_{tag}_malpha": np_(malpha), f"nn_{tag}_nqp": np_(nqp)})
+    save("stepgen_f64", **out)
+
+
+# --------------------------------------------------------------------------
 # L. the 5-parameter pendulum (pendulum.py simple=False, il_env.py:40-42
 #    'pendulum-complex'): forward, its autograd Jacobian (the reference's own
 #    closed forms unpack three parameters and fail for it), and MPC solves
@@ -764,10 +825,10 @@ def case_complex():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["models", "riccati", "pnqp", "lqrstep", "mpc", "adjoint", "implicit",
-                             "datasets", "il", "generic", "api", "complex"]
+                             "datasets", "il", "generic", "api", "complex", "stepgen"]
     table = {"models": case_models, "riccati": case_riccati, "pnqp": case_pnqp,
              "lqrstep": case_lqrstep, "mpc": case_mpc, "adjoint": case_classic_adjoint,
              "implicit": case_implicit, "datasets": case_datasets, "il": case_il,
-             "generic": case_generic, "api": case_api, "complex": case_complex}
+             "generic": case_generic, "api": case_api, "complex": case_complex, "stepgen": case_stepgen}
     for w in which:
         table[w]()

@@ -159,3 +159,47 @@ def test_delta_u_trust_region(golden):
         x, u, costs = m(gpu(g["cart_auto_x0"]), dilqr.QuadCost(C, c), dx)
     assert relerr(cpu(costs), g["delta_u_costs"]) < 1e-3
     assert relerr(cpu(u), g["delta_u_u"]) < 1e-3
+
+
+@pytest.mark.parametrize("variant", ["explicit", "classic"])
+@pytest.mark.parametrize("case", ["nq", "nn"])
+def test_lqrstep_generic_true_cost_and_dynamics(golden, variant, case):
+    """One LQRStep forward (both variants) whose line search evaluates a
+    non-quadratic true_cost (pendulum, "nq") or a Module true_dynamics
+    (NNDynamics, "nn"), lqr_step_explicit.py:226-236 / lqr_step.py:224-234:
+    the HIP Riccati sweep, the rollout in torch.  Against the reference's fp64
+    step on the same inputs (case M of gen_golden.py): new x, u, costs,
+    full_du_norm, mean step size and the pnqp iteration count."""
+    import dilqr
+    import dilqr.lqr_step as classic
+    g = golden("stepgen_f64")
+    mod = dilqr if variant == "explicit" else classic
+    if case == "nq":
+        from dilqr.env_dx.pendulum import PendulumDx
+        T, B = g["nq_u"].shape[:2]
+        dx = PendulumDx()
+        q, p = dx.get_true_obj()
+        C, c = torch.diag(q).repeat(T, B, 1, 1).to(DEV), p.repeat(T, B, 1).to(DEV)
+        cost, lo, hi, mls = NQCost(gpu(g["nq_w"])), -2.0, 2.0, 5
+    else:
+        from dilqr.dynamics import NNDynamics
+        T, B = g["nn_u"].shape[:2]
+        dx = NNDynamics(5, 1, hidden_sizes=[32], activation="sigmoid").to(DEV)
+        with torch.no_grad():
+            for i, fc in enumerate(dx.fcs):
+                fc.weight.copy_(gpu(g[f"nn_W{i}"]))
+                fc.bias.copy_(gpu(g[f"nn_b{i}"]))
+        C, c = gpu(g["nn_C"]), gpu(g["nn_c"])
+        cost, lo, hi, mls = dilqr.QuadCost(C, c), -1.0, 1.0, 10
+    X, U = gpu(g[f"{case}_X"]), gpu(g[f"{case}_u"])
+    step = mod.LQRStep(X.shape[2], 1, T, u_lower=lo, u_upper=hi, true_cost=cost, true_dynamics=dx, current_x=X,
+                       current_u=U, linesearch_decay=0.2, max_linesearch_iter=mls)
+    args = (gpu(g[f"{case}_x0"]), C, c, gpu(g[f"{case}_F"]), gpu(g[f"{case}_f"]))
+    with torch.no_grad():
+        nx, nu, nqp, costs, du, malpha = step(*args, None) if variant == "explicit" else step(*args)
+    k = f"{case}_{variant}"
+    errs = {name: relerr(cpu(a), g[f"{k}_{name}"]) for name, a in
+            (("nx", nx), ("nu", nu), ("costs", costs), ("du", du), ("malpha", malpha))}
+    print(f"\n[LQRStep {variant} {case}] " + ", ".join(f"{a} {b:.2e}" for a, b in errs.items()))
+    assert max(errs.values()) < 1e-4, errs
+    assert float(nqp[0]) == float(g[f"{k}_nqp"][0])
