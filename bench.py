@@ -185,7 +185,7 @@ def sweep_roofline(n, m, T, B, dev, reps=5):
     nb = N.Bounds(N.BOUNDS_NONE, 0.0, 0.0, None, None)
     s = N.stream(dev)
     call = lambda r: N.call("dilqr_lqr_backward_f32", n, m, T, B, N.ptr(C), N.ptr(cb), None, None, N.ptr(F), nb,
-                            None, 0, N.ptr(K), N.ptr(k), None, s)
+                            None, 0, N.ptr(K), N.ptr(k), None, None, s)
     call(0)
     ms = _event_ms(torch.cuda.current_stream(dev), call, reps)
     d = n + m
@@ -683,7 +683,7 @@ def main():
     nb = N.Bounds(N.BOUNDS_NONE, 0.0, 0.0, None, None)
     sweep = lambda r: N.call(  # noqa: E731
         "dilqr_lqr_backward_f32", N_STATE, N_CTRL, T_HORIZON, B, N.ptr(C), N.ptr(cb), None, None, N.ptr(F), nb, None,
-        0, N.ptr(K), N.ptr(k), None, s)
+        0, N.ptr(K), N.ptr(k), None, None, s)
     sweep(0)            # the first launch from this unit's code object loads it (~ms): keep it out of the timing
     sweep_ms = _event_ms(stream, sweep, reps)
     sweep_bytes = SWEEP_BYTES_PER_PROBLEM * B

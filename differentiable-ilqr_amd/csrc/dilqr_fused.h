@@ -685,7 +685,7 @@ struct LaneIter {
   int slot;                                                 // the accepted candidate's slot
 };
 
-template <class Model, int BM, bool LG, bool FIRST, bool PREV = true>
+template <class Model, int BM, bool LG, bool FIRST, bool PREV = true, int GS = kBlock>
 DEV LaneIter mpc_iteration_lane(int T, int B, int b, const Model md, const float* __restrict__ x_init,
                                 const float* __restrict__ C, const float* __restrict__ c, const Bounds& bd,
                                 float decay, int max_ls, const MpcState& S, float* __restrict__ du_sq,
@@ -700,7 +700,7 @@ DEV LaneIter mpc_iteration_lane(int T, int B, int b, const Model md, const float
   float* xsb = S.Xs + sb * TBd;
   float cost, alpha;
   int win;
-  const GainRecs gr = LG ? GainRecs{lds_gains, kBlock, (int)threadIdx.x} : GainRecs{S.ws, B, b};
+  const GainRecs gr = LG ? GainRecs{lds_gains, GS, (int)threadIdx.x} : GainRecs{S.ws, B, b};
   // the solve's packed symmetric cost: built by iteration 0's sweep (which reads
   // C, c), used from iteration 1 on by every problem whose C_t are all bitwise
   // symmetric, reading only diag(C_t) and c_t when they are all diagonal too
@@ -1015,21 +1015,34 @@ DEV void mpc_reset_ctrl(const MpcState& S) {
 // only trajectory records it wrote itself, and the gain records in LDS are its
 // own, so no barrier is involved; every lane's loop runs exactly `iters`
 // iterations and exits.
+// Occupancy experiment builds only (tools/gpu_occupancy_exp.sh;
+// never the shipped library): kSolveLpw problems per 64-lane wave (32: half the
+// lanes idle, twice the waves) and a launch-bounds floor of DILQR_SOLVE_OCC
+// waves per SIMD (2: at most 256 registers per lane), so that two waves of the
+// same per-lane code are co-resident on a SIMD with their gain records in LDS.
+#ifndef DILQR_SOLVE_LPW
+#define DILQR_SOLVE_LPW 64
+#endif
+#ifndef DILQR_SOLVE_OCC
+#define DILQR_SOLVE_OCC 1
+#endif
+constexpr int kSolveLpw = DILQR_SOLVE_LPW;
+
 template <class Model, int BM, bool LG>
-__global__ void __launch_bounds__(kBlock) k_mpc_solve_fixed(int T, int B, const float* __restrict__ theta,
+__global__ void __launch_bounds__(kBlock, DILQR_SOLVE_OCC) k_mpc_solve_fixed(int T, int B, const float* __restrict__ theta,
                                                             const float* __restrict__ x_init,
                                                             const float* __restrict__ u_init,
                                                             const float* __restrict__ C, const float* __restrict__ c,
                                                             Bounds bd, float decay, int max_ls, int iters,
                                                             float best_cost_eps, MpcState S) {
   constexpr int m = Model::M;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.x * kSolveLpw + threadIdx.x;
   // diagnostic stamps (tools/phase_stamps.py solve): 0/6 entry, 1 begin done,
   // 3 iteration 0 done, 4 last iteration starts, 2 its sweep done, 5/7 exit
   DILQR_STAMP(0);
   DILQR_STAMP(6);
   if (b == 0) mpc_reset_ctrl(S);
-  if (b >= B) return;
+  if (b >= B || (int)threadIdx.x >= kSolveLpw) return;
   Model md; md.load(theta);
   extern __shared__ __attribute__((aligned(16))) float lds_gains[];
   // begin; with a packed copy it also reads C once and sets the cost flags, and
@@ -1039,8 +1052,9 @@ __global__ void __launch_bounds__(kBlock) k_mpc_solve_fixed(int T, int B, const 
   const unsigned pk = S.Cpk ? mpc_begin_lane<Model, true>(T, B, b, md, x_init, u_init, S, C, c)
                             : mpc_begin_lane<Model>(T, B, b, md, x_init, u_init, S);
   DILQR_STAMP(1);
-  LaneIter r = mpc_iteration_lane<Model, BM, LG, false, false>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
-                                                               S.du_sq, lds_gains, 0, 0, pk, 0.f);
+  LaneIter r = mpc_iteration_lane<Model, BM, LG, false, false, kSolveLpw>(T, B, b, md, x_init, C, c, bd, decay,
+                                                                          max_ls, S, S.du_sq, lds_gains, 0, 0, pk,
+                                                                          0.f);
   int cur = r.slot, best = r.slot, best_iter = 0;
   float best_cost = r.cost;
   bool take = true;
@@ -1048,8 +1062,9 @@ __global__ void __launch_bounds__(kBlock) k_mpc_solve_fixed(int T, int B, const 
   const size_t plane = (size_t)T * m * B;                   // one iteration's du rows
   for (int it = 1; it < iters; ++it) {
     if (it == iters - 1) DILQR_STAMP(4);
-    r = mpc_iteration_lane<Model, BM, LG, false>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
-                                                 S.du_sq + it * plane, lds_gains, cur, best, pk, r.cost);
+    r = mpc_iteration_lane<Model, BM, LG, false, true, kSolveLpw>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
+                                                                  S.du_sq + it * plane, lds_gains, cur, best, pk,
+                                                                  r.cost);
     take = mpc_takes_best(false, r.cost, best_cost, best_cost_eps);
     if (take) { best_cost = r.cost; best = r.slot; best_iter = it; }
     cur = r.slot;
@@ -1115,12 +1130,13 @@ template <class MD>
 int launch_mpc_solve_tpp(const MpcSolveArgs& a) {
 #define LAUNCH_SOLVE(BM_)                                                                                    \
   do {                                                                                                       \
-    const size_t lds = (size_t)a.T * kBlock * (MD::N * MD::M + MD::M) * sizeof(float);                      \
-    if (lds_gains_fit(lds, a.B))                                                                             \
-      k_mpc_solve_fixed<MD, BM_, true><<<grid_for(a.B), kBlock, lds, a.stream>>>(                             \
+    const size_t lds = (size_t)a.T * kSolveLpw * (MD::N * MD::M + MD::M) * sizeof(float);                   \
+    const int grid = (int)(((long long)a.B + kSolveLpw - 1) / kSolveLpw);                                   \
+    if (lds_gains_fit(lds * kBlock / kSolveLpw, a.B))                                                       \
+      k_mpc_solve_fixed<MD, BM_, true><<<grid, kBlock, lds, a.stream>>>(                                      \
           a.T, a.B, a.theta, a.x_init, a.u_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iters, a.best_cost_eps, a.st); \
     else                                                                                                     \
-      k_mpc_solve_fixed<MD, BM_, false><<<grid_for(a.B), kBlock, 0, a.stream>>>(                              \
+      k_mpc_solve_fixed<MD, BM_, false><<<grid, kBlock, 0, a.stream>>>(                                       \
           a.T, a.B, a.theta, a.x_init, a.u_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iters, a.best_cost_eps, a.st); \
   } while (0)
   if (a.bd.mode == DILQR_BOUNDS_TENSOR) LAUNCH_SOLVE(DILQR_BOUNDS_TENSOR);

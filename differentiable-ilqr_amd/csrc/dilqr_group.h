@@ -416,7 +416,7 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
                                                            const float* __restrict__ u, const float* __restrict__ F,
                                                            Bounds bd, const unsigned char* __restrict__ zI,
                                                            float* __restrict__ K, float* __restrict__ k,
-                                                           int* __restrict__ n_qp) {
+                                                           int* __restrict__ n_qp, int* __restrict__ n_qp_step) {
   constexpr int d = n + m;
   using LdsT = GroupLdsT<n, m, true, true>;
   __shared__ LdsT Ls[kGPW];
@@ -473,8 +473,10 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
       }
     }
     float col[m];
+    const int qp_before = nqp;
     group_riccati_step_t<n, m, MODE, DenseF, LAST>(L, r, FRows<n, m>{L}, U, Crow, cb, zIt, lb, ub, col, prev_k,
                                                    have_prev, nqp);
+    if (MODE == GAIN_BOX && valid && n_qp_step && r == 0) atomicMax(n_qp_step + t, nqp - qp_before - 1);
     if (valid) {
       if (r < n) {
 #pragma unroll

@@ -13,7 +13,7 @@ __global__ void __launch_bounds__(kBlock) k_lqr_backward(int T, int B, const flo
                                                          const float* __restrict__ u, const float* __restrict__ F,
                                                          Bounds bd, const unsigned char* __restrict__ zI,
                                                          float* __restrict__ K, float* __restrict__ k,
-                                                         int* __restrict__ n_qp) {
+                                                         int* __restrict__ n_qp, int* __restrict__ n_qp_step) {
   constexpr int d = n + m;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
@@ -77,8 +77,10 @@ __global__ void __launch_bounds__(kBlock) k_lqr_backward(int T, int B, const flo
     }
     float Kt[m][n], kt[m];
     symsofar &= bitwise_symmetric(cur.C);              // the fused sweep's rule (RiccatiState SYM)
+    const int qp_before = rs.n_qp;
     if (symsofar) rs.template step<MODE, DenseF, false, true>(cur.C, cb, cur.F, zIt, lb, ub, Kt, kt);
     else rs.template step<MODE>(cur.C, cb, cur.F, zIt, lb, ub, Kt, kt);
+    if (MODE == GAIN_BOX && n_qp_step) atomicMax(n_qp_step + t, rs.n_qp - qp_before - 1);
     st2(K + tb * m * n, Kt);
     st(k + tb * m, kt);
     cur = nxt;
@@ -94,7 +96,7 @@ extern "C" {
 
 int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const float* c, const float* x,
                            const float* u, const float* F, dilqr_bounds bounds, const unsigned char* u_zero_I,
-                           int m_solver, float* K, float* k, int* n_qp_iter, void* stream) {
+                           int m_solver, float* K, float* k, int* n_qp_iter, int* n_qp_step, void* stream) {
   if (T < 1 || B < 0 || !C || !c || !K || !k || (T > 1 && !F)) return DILQR_E_ARG;
   if (x && !u) return DILQR_E_ARG;   // u alone: c is already c_back, u only shifts the bounds
   if (!al16(C) || !al16(c) || !al16(x) || !al16(u) || !al16(F) || !al16(K) || !al16(k)) return DILQR_E_ARG;
@@ -109,7 +111,8 @@ int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const flo
              : u_zero_I ? GAIN_ZERO_I
              : (m_solver == DILQR_SOLVE_CHOL && m > 1) ? GAIN_CHOL : GAIN_UNC;
 #define LAUNCH(N_, M_, MODE_) \
-  k_lqr_backward<N_, M_, MODE_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, C, c, x, u, F, bd, u_zero_I, K, k, n_qp_iter)
+  k_lqr_backward<N_, M_, MODE_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, C, c, x, u, F, bd, u_zero_I, K, k, n_qp_iter, \
+                                                                       n_qp_step)
 #define X(N_, M_)                                              \
   if (n == N_ && m == M_) {                                    \
     switch (mode) {                                            \
@@ -124,7 +127,7 @@ int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const flo
 #undef LAUNCH
 #define LAUNCH(N_, M_, MODE_)                                                                                     \
   k_lqr_backward_group<N_, M_, MODE_><<<grid_group(B), 64, 0, S(stream)>>>(T, B, C, c, x, u, F, bd, u_zero_I, K, k, \
-                                                                           n_qp_iter)
+                                                                           n_qp_iter, n_qp_step)
   DILQR_FOR_EACH_GROUP_SHAPE(X)
 #undef X
 #undef LAUNCH

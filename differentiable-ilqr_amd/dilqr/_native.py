@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must be imported first: libdilqr.so then binds to t
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DILQR_LIB", os.path.join(_HERE, "libdilqr.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 _PKG = os.path.dirname(_HERE)          # differentiable-ilqr_amd/ (the Makefile's directory)
 
 MODEL_LINDX, MODEL_PENDULUM, MODEL_CARTPOLE, MODEL_ROCKET, MODEL_PENDULUM_COMPLEX = 0, 1, 2, 3, 4
@@ -49,7 +49,7 @@ SIGNATURES = {
     "dilqr_rollout_f32": ([_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_linearize_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_lqr_backward_f32": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, Bounds, _vp, _i, _vp, _vp, _vp,
-                                _vp], _i),
+                                _vp, _vp], _i),
     "dilqr_lqr_forward_f32": ([_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, Bounds,
                                _vp, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_pnqp_f32": ([_i, _i, _vp, _vp, Bounds, _vp, _vp, _vp, _vp, _vp, _vp], _i),

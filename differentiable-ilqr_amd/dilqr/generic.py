@@ -233,10 +233,10 @@ def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u
         # +-delta_u (exact values), c_back formed here
         rlo, rhi = ops.delta_u_sweep_bounds(lo, hi, ud, delta_u)
         K, k, nqp = ops.lqr_backward(Cd, ops.c_back(Cd, cd, xd, ud), Fd, n, m, u_lower=rlo, u_upper=rhi,
-                                     want_nqp=extras)
+                                     qp_total=extras)
     else:
         K, k, nqp = ops.lqr_backward(Cd, cd, Fd, n, m, x=xd, u=ud, u_lower=lo, u_upper=hi,
-                                     u_zero_I=zI if lo is None else None, want_nqp=extras and lo is not None)
+                                     u_zero_I=zI if lo is None else None, qp_total=extras and lo is not None)
     old_cost = traj_cost(T, x, u, true_cost)
     alphas = torch.ones(B, device=x.device)
     cur_cost, full_du_norm = None, None
@@ -283,7 +283,7 @@ def lqr_step_forward(T, n, m, x_init, C, c, F, x, u, true_cost, true_dynamics, u
         if extras:
             alphas = torch.where(cur_cost > old_cost, alphas / decay, alphas)
     if extras:
-        n_qp = int(nqp.max().item()) if nqp is not None else 0
+        n_qp = nqp if isinstance(nqp, int) else 0
         return new_x, new_u, cur_cost, full_du_norm, alphas, n_qp
     return new_x, new_u, cur_cost, full_du_norm
 

@@ -44,10 +44,10 @@ def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta
             if delta_u is not None:                             # lqr_step.py:130-135
                 rlo, rhi = ops.delta_u_sweep_bounds(lo, hi, u, delta_u)
                 K, k, nqp = ops.lqr_backward(C, ops.c_back(C.detach(), c.detach(), x, u), F, n_state, n_ctrl,
-                                             u_lower=rlo, u_upper=rhi, want_nqp=True)
+                                             u_lower=rlo, u_upper=rhi, qp_total=True)
             else:
                 K, k, nqp = ops.lqr_backward(C, c, F, n_state, n_ctrl, x=x, u=u, u_lower=lo, u_upper=hi,
-                                             u_zero_I=zI if lo is None else None, want_nqp=lo is not None)
+                                             u_zero_I=zI if lo is None else None, qp_total=lo is not None)
             if m_id == N.MODEL_LINDX:
                 th, Fd, fd = None, true_dynamics.F, true_dynamics.f
                 if fd is not None and fd.nelement() == 0:
@@ -60,7 +60,7 @@ def LQRStep(n_state, n_ctrl, T, u_lower=None, u_upper=None, u_zero_I=None, delta
                 m_id, th, x_init, Ct, ct, x, u, K, k, F=Fd, f=fd, u_lower=flo, u_upper=fhi, u_zero_I=zI,
                 linesearch_decay=linesearch_decay, max_linesearch_iter=max_linesearch_iter)
             full_du_norm = ops.quirk_norm(du_sq)
-            n_qp = int(nqp.max().item()) if nqp is not None else 0
+            n_qp = nqp if isinstance(nqp, int) else 0
             ctx.save_for_backward(x_init, C, c, F, f, nx, nu)
             return nx, nu, torch.tensor([float(n_qp)]), costs, full_du_norm, alphas.mean()
 

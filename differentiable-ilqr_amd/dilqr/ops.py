@@ -75,9 +75,13 @@ def zero_mask(u_zero_I, T, B, m, device):
 
 
 def lqr_backward(C, c, F, n, m, x=None, u=None, u_lower=None, u_upper=None, u_zero_I=None,
-                 m_solver=N.SOLVE_INV, want_nqp=False):
+                 m_solver=N.SOLVE_INV, want_nqp=False, qp_total=False):
     """lqr_backward (lqr_step_explicit.py:54-162) with the fused delta-space c_back.
-    Returns K [T,B,m,n], k [T,B,m] (natural time order), n_qp [B] or None."""
+    Returns K [T,B,m,n], k [T,B,m] (natural time order), and n_qp [B] (the
+    per-problem sums of 1 + pnqp iterations) with want_nqp, or with qp_total
+    the reference's n_total_qp_iter (lqr_step_explicit.py:148-150: its batched
+    pnqp runs each step until the slowest problem converges, so the count is
+    sum_t (1 + max over problems of that step's iterations); 0 unbounded)."""
     T, B = C.shape[:2]
     C, c, F, x, u = _f32(C), _f32(c), _f32(F), _f32(x), _f32(u)
     bounds, keep = N.make_bounds(u_lower, u_upper)
@@ -85,9 +89,12 @@ def lqr_backward(C, c, F, n, m, x=None, u=None, u_lower=None, u_upper=None, u_ze
     K = torch.empty(T, B, m, n, device=C.device)
     k = torch.empty(T, B, m, device=C.device)
     nqp = torch.zeros(B, dtype=torch.int32, device=C.device) if want_nqp else None
+    step = torch.zeros(T, dtype=torch.int32, device=C.device) if qp_total else None
     N.call("dilqr_lqr_backward_f32", n, m, T, B, N.ptr(C), N.ptr(c), N.ptr(x), N.ptr(u), N.ptr(F), bounds,
-           N.ptr(zI), m_solver, N.ptr(K), N.ptr(k), N.ptr(nqp), N.stream(C.device))
+           N.ptr(zI), m_solver, N.ptr(K), N.ptr(k), N.ptr(nqp), N.ptr(step), N.stream(C.device))
     del keep
+    if qp_total:
+        return K, k, (int(step.sum().item()) + T if bounds.mode != N.BOUNDS_NONE else 0)
     return K, k, nqp
 
 

@@ -67,7 +67,7 @@ typedef struct dilqr_bounds {
   const float* hi_t;             /* [T,B,m] or NULL                              */
 } dilqr_bounds;
 
-/* Library version (for the loader's sanity check): 7. */
+/* Library version (for the loader's sanity check): 8. */
 int dilqr_version(void);
 
 /* Build id: the first 16 hex digits of the sha256 of the sources the library
@@ -119,12 +119,16 @@ int dilqr_linearize_f32(int model, int T, int B, const float* theta, const float
    run pnqp (pnqp.py:5-82) per step, warm-started from the later step.
    u_zero_I [T,B,m] (uint8, nullable): the masked solve of
    lqr_step_backup.py:210-232 used by the adjoint engines.
-   n_qp_iter [B] (nullable): per-problem sum of 1+pnqp iterations. */
+   n_qp_iter [B] (nullable): per-problem sum of 1+pnqp iterations.
+   n_qp_step [T] (nullable, zeroed by the caller): per step, the largest pnqp
+   iteration count over the batch (atomic max) — the reference's batched pnqp
+   runs until its slowest problem converges, so its n_total_qp_iter
+   (lqr_step_explicit.py:148-150) is sum_t (1 + n_qp_step[t]). */
 int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const float* c,
                            const float* x, const float* u, const float* F,
                            dilqr_bounds bounds, const unsigned char* u_zero_I,
                            int m_solver, float* K, float* k, int* n_qp_iter,
-                           void* stream);
+                           int* n_qp_step, void* stream);
 
 /* Rollout with per-problem backtracking line search: lqr_forward,
    lqr_step_explicit.py:166-263.  `model` gives the true dynamics (F/f for

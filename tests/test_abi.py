@@ -57,17 +57,18 @@ def test_invalid_arguments_rejected_without_launch():
     lib = N.lib()
     nb = N.Bounds(N.BOUNDS_NONE, 0.0, 0.0, None, None)
     # null C
-    rc = lib.dilqr_lqr_backward_f32(5, 1, 25, 8, None, None, None, None, None, nb, None, 0, None, None, None, None)
+    rc = lib.dilqr_lqr_backward_f32(5, 1, 25, 8, None, None, None, None, None, nb, None, 0, None, None, None, None,
+                                    None)
     assert rc == 2
     # misaligned pointer
     rc = lib.dilqr_lqr_backward_f32(5, 1, 25, 8, ctypes.c_void_p(4), ctypes.c_void_p(16), None, None,
                                     ctypes.c_void_p(16), nb, None, 0, ctypes.c_void_p(16), ctypes.c_void_p(16),
-                                    None, None)
+                                    None, None, None)
     assert rc == 2
     # unsupported (n, m)
     rc = lib.dilqr_lqr_backward_f32(11, 5, 25, 8, ctypes.c_void_p(16), ctypes.c_void_p(16), None, None,
                                     ctypes.c_void_p(16), nb, None, 0, ctypes.c_void_p(16), ctypes.c_void_p(16),
-                                    None, None)
+                                    None, None, None)
     assert rc == 1
     # unknown model
     rc = lib.dilqr_dynamics_f32(42, 4, ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16),
