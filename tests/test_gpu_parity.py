@@ -1,11 +1,15 @@
 """GPU parity: the HIP path (through the C-ABI) against the oracle and the
 reference's golden vectors.
 
-Tolerances (fp32 kernels vs fp64 oracle on identical inputs):
-  * pointwise dynamics / Jacobians:  rtol 2e-5 (atan2/sin/cos ulp differences)
-  * one Riccati sweep:               rtol 1e-4 (north-star bar)
-  * solver outputs (trajectories):   rtol 1e-4 on costs; trajectories 1e-3 abs
-    (discrete line-search/active-set decisions are re-made in fp32)
+Tolerances (fp32 kernels vs fp64 oracle / the reference's fp64 goldens on
+identical inputs; every bar is relative to the array's max magnitude):
+  * pointwise dynamics / Jacobians:  2e-5 / 5e-5 (atan2/sin/cos ulp differences)
+  * Riccati sweeps, pnqp, rollouts, adjoint and implicit gradients: 1e-4 (the
+    north-star bar; measured errors are printed, round 4: <= 2.5e-6)
+  * MPC solves: by decision replay (check_against_forced_oracle) — the fp64
+    oracle made to take the GPU's line-search / best-iterate decisions must
+    reproduce its trajectories within 1e-4, and every decision the oracle makes
+    differently on its own must be a near-tie (margin < 1e-5)
 """
 import numpy as np
 import pytest
@@ -470,8 +474,19 @@ def test_classic_adjoint_vs_golden(golden, tag, bounds):
     assert relerr(cpu(x), g[f"{tag}_x"]) < 1e-4 and relerr(cpu(u), g[f"{tag}_u"]) < 1e-4
     loss = (x * gpu(g[f"{tag}_wx"])).sum() + (u * gpu(g[f"{tag}_wu"])).sum()
     loss.backward()
-    for key, t in (("dx0", x0t), ("dC", Ct), ("dc", ct), ("dF", Ft), ("df", ft)):
-        assert relerr(cpu(t.grad), g[f"{tag}_{key}"]) < 1e-3, key
+    # the adjoint kernel alone: the oracle's backward at the GPU's own solution
+    xg, ug = cpu(x), cpu(u)
+    od = oadj.classic_backward(g[f"{tag}_wx"], g[f"{tag}_wu"], x0, C, c, F, f, xg, ug, lo, hi)
+    e_own = {k: relerr(cpu(t.grad), o) for (k, t), o in zip((("dx0", x0t), ("dC", Ct), ("dc", ct), ("dF", Ft),
+                                                             ("df", ft)), od)}
+    e_ref = {k: relerr(cpu(t.grad), g[f"{tag}_{k}"]) for k, t in (("dx0", x0t), ("dC", Ct), ("dc", ct),
+                                                                   ("dF", Ft), ("df", ft))}
+    print(f"\n[classic adjoint {tag}] x {relerr(xg, g[f'{tag}_x']):.2e} u {relerr(ug, g[f'{tag}_u']):.2e}; "
+          f"at the GPU solution: " + ", ".join(f"{k} {v:.2e}" for k, v in e_own.items()) +
+          "; vs the golden: " + ", ".join(f"{k} {v:.2e}" for k, v in e_ref.items()))
+    # measured (round 4): <= 2.5e-7 at the GPU's solution, <= 7.2e-7 against the golden
+    assert max(e_own.values()) < 1e-5, e_own
+    assert max(e_ref.values()) < 1e-4, e_ref
 
 
 # ------------------------------------------------------------------ the reference's datasets
@@ -790,7 +805,7 @@ def test_implicit_backward_rocket_full_size(bounds):
     """Config 3 shape (rocket T=30, B=32768) through the 16-lane implicit kernel:
     finite gradients, a 64-problem slice gives bit-identical per-problem results,
     and a small slice matches the oracle's fast algebra run on the same fp32
-    solution (fp64 oracle, 1e-3 of the max magnitude: the GPU works in fp32)."""
+    solution (fp64 oracle, 1e-4 of the max magnitude)."""
     from dilqr import ops
     from dilqr.implicit import implicit_backward
     B, T, n, m = 32768, 30, 13, 3
@@ -818,9 +833,11 @@ def test_implicit_backward_rocket_full_size(bounds):
     K_rev = f64(K)[::-1].copy()
     rdC, rdc, rdth = oadj.implicit_backward_fast(omodels.Rocket, f64(wx), f64(wu), f64(C), f64(c), f64(F), None,
                                                  f64(x), f64(u), K_rev, lo, hi)
-    assert relerr(cpu(dth[so]), rdth) < 1e-3
-    assert relerr(cpu(dc[:, so]), rdc) < 1e-3
-    assert relerr(cpu(dC[:, so]), rdC) < 1e-3
+    print(f"\n[rocket implicit full size {bounds}] vs fp64 oracle: dtheta {relerr(cpu(dth[so]), rdth):.2e}, "
+          f"dc {relerr(cpu(dc[:, so]), rdc):.2e}, dC {relerr(cpu(dC[:, so]), rdC):.2e}")
+    assert relerr(cpu(dth[so]), rdth) < 1e-4          # measured (round 4): <= 1.6e-6
+    assert relerr(cpu(dc[:, so]), rdc) < 1e-4
+    assert relerr(cpu(dC[:, so]), rdC) < 1e-4
 
 
 # ------------------------------------------------------------------ 16-lanes-per-problem kernels (rocket)
@@ -843,10 +860,15 @@ def test_riccati_group_rocket_vs_golden(golden, variant):
     elif variant == "box_":
         kw = dict(u=gpu(u), u_lower=-1.0, u_upper=1.0)
     K, k, _ = ops.lqr_backward(gpu(C), gpu(c), gpu(F), n, m, **kw)
-    # pnqp's m=3 active-set solves amplify fp32 rounding (measured 1.4e-4 on k)
-    tol = 1e-3 if variant == "box_" else 1e-4
+    # measured (round 4): per-problem errors <= 1e-6 on k and K in every variant
+    tol = 1e-4
     if variant == "box_":
-        Ko, ko, _ = olqr.lqr_backward(C, c, F, n, m, u=u, u_lower=-1.0, u_upper=1.0, per_problem=True)
+        mg = {}
+        Ko, ko, _ = olqr.lqr_backward(C, c, F, n, m, u=u, u_lower=-1.0, u_upper=1.0, per_problem=True, margins=mg)
+        ek = np.abs(cpu(k) - ko).max(axis=(0, 2)) / max(1.0, np.abs(ko).max())
+        eK = np.abs(cpu(K) - Ko).max(axis=(0, 2, 3)) / max(1.0, np.abs(Ko).max())
+        print(f"\n[rocket box riccati] per problem k err {np.array2string(ek, precision=1)}, K err "
+              f"{np.array2string(eK, precision=1)}, pnqp margins {np.array2string(mg.get('pnqp'), precision=1)}")
         assert relerr(cpu(K), Ko) < tol and relerr(cpu(k), ko) < tol
     assert relerr(cpu(K), g[f"rocket_{variant}K"]) < tol
     assert relerr(cpu(k), g[f"rocket_{variant}k"]) < tol
@@ -886,9 +908,13 @@ def test_lqr_forward_group_vs_oracle(dyn, bounds):
     nx, nu, cost, _, _ = ops.lqr_forward(mid, ops.theta_of(dx, gpu(x0)), gpu(x0), gpu(C), gpu(c), gpu(x), gpu(u),
                                          gpu(Ko), gpu(ko), F=gpu(F), f=gpu(f), u_lower=lo, u_upper=hi,
                                          linesearch_decay=0.2, max_linesearch_iter=5)
-    assert relerr(cpu(cost), co) < 1e-4
-    assert relerr(cpu(nu), uo) < 1e-3
-    assert relerr(cpu(nx), xo) < 1e-3
+    uerr = np.abs(cpu(nu) - uo).max(axis=(0, 2)) / max(1.0, np.abs(uo).max())
+    xerr = np.abs(cpu(nx) - xo).max(axis=(0, 2)) / max(1.0, np.abs(xo).max())
+    print(f"\n[group LS {dyn} {bounds}] cost {relerr(cpu(cost), co):.2e}; u per problem max {uerr.max():.2e} "
+          f"(worst {np.argsort(-uerr)[:3]} {np.sort(uerr)[-3:]}), x max {xerr.max():.2e}")
+    assert relerr(cpu(cost), co) < 1e-4                # measured (round 4): <= 2.6e-7, u and x <= 1.1e-6
+    assert relerr(cpu(nu), uo) < 1e-4
+    assert relerr(cpu(nx), xo) < 1e-4
 
 
 def test_rocket_fused_iteration_equals_unfused(golden):
@@ -995,9 +1021,16 @@ def test_fused_iteration_vs_oracle(model, bounds, decay, mls):
     same = np.abs(cpu(alpha) - ao) < 1e-6 * np.maximum(1, ao)
     assert same[clear].all(), np.flatnonzero(clear & ~same)
     cerr = np.abs(cpu(cost) - co) / np.maximum(1.0, np.abs(co))
-    assert np.median(cerr[same]) < 1e-5 and np.max(cerr[same]) < 1e-3
-    assert relerr(cpu(nu)[:, same], uo[:, same]) < 1e-3
-    assert relerr(cpu(nx)[:, same], xo[:, same]) < 1e-3
+    uerr = np.abs(cpu(nu) - uo).max(axis=(0, 2)) / max(1.0, np.abs(uo).max())
+    xerr = np.abs(cpu(nx) - xo).max(axis=(0, 2)) / max(1.0, np.abs(xo).max())
+    print(f"\n[fused vs oracle {model} {bounds}] same {same.sum()}/{B}, clear {clear.sum()}; cost max "
+          f"{cerr[same].max():.2e} med {np.median(cerr[same]):.2e}; u max {uerr[same].max():.2e}, x max "
+          f"{xerr[same].max():.2e}; worst problems u {np.argsort(-uerr * same)[:4]} "
+          f"{np.sort(uerr[same])[-4:]}")
+    # measured (round 4): costs <= 1.8e-5, u and x <= 2.5e-6 on the problems with the oracle's step size
+    assert np.median(cerr[same]) < 1e-5 and np.max(cerr[same]) < 1e-4
+    assert relerr(cpu(nu)[:, same], uo[:, same]) < 1e-4
+    assert relerr(cpu(nx)[:, same], xo[:, same]) < 1e-4
 
 
 # ------------------------------------------------------------------ standalone pnqp (a4)
@@ -1011,12 +1044,23 @@ def test_pnqp_standalone_vs_golden(golden, m):
     H, q, lo, hi, x0 = (g[f"m{m}_{k}"] for k in ("H", "q", "lo", "hi", "x0"))
     x, Hf, If, it = ops.pnqp(gpu(H), gpu(q), gpu(lo), gpu(hi))
     assert relerr(cpu(x), g[f"m{m}_x_pp"]) < 1e-4
-    assert np.mean(cpu(it) == g[f"m{m}_it_pp"]) > 0.95       # exit index: fp32 near-ties at 1e-4
+    mg = {}
+    olqr.pnqp(H, q, lo, hi, per_problem=True, margins=mg)
+    dif = cpu(it) != g[f"m{m}_it_pp"]
+    print(f"\n[pnqp m={m}] x {relerr(cpu(x), g[f'm{m}_x_pp']):.2e}; exit index differs on {dif.sum()}/{len(dif)}, "
+          f"their decision margins {np.array2string(mg['pnqp'][dif], precision=1)}; smallest margin elsewhere "
+          f"{mg['pnqp'][~dif].min():.1e}")
+    # exit index: equal, except on a decision within 1e-4 of its threshold (the stop
+    # test |dx| < 1e-4 sits there); measured (round 4): equal on every problem
+    assert dif.sum() <= 2 and np.all(mg["pnqp"][dif] < 1e-4), np.flatnonzero(dif)
     x2, Hf2, If2, it2 = ops.pnqp(gpu(H), gpu(q), -0.7, 0.7, x_init=gpu(x0))
-    xo, Hfo, Ifo, ito = olqr.pnqp(H, q, -0.7, 0.7, x_init=x0, per_problem=True)
+    mg2 = {}
+    xo, Hfo, Ifo, ito = olqr.pnqp(H, q, -0.7, 0.7, x_init=x0, per_problem=True, margins=mg2)
     assert relerr(cpu(x2), xo) < 1e-4
     same = cpu(it2) == ito
-    assert np.mean(same) > 0.95
+    print(f"[pnqp m={m} warm] x {relerr(cpu(x2), xo):.2e}; exit index differs on {(~same).sum()}, margins "
+          f"{np.array2string(mg2['pnqp'][~same], precision=1)}")
+    assert (~same).sum() <= 2 and np.all(mg2["pnqp"][~same] < 1e-4), np.flatnonzero(~same)
     assert np.array_equal(cpu(If2)[same], Ifo[same])
     assert relerr(cpu(Hf2)[same], Hfo[same]) < 1e-5
 
