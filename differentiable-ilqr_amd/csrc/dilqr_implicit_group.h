@@ -62,6 +62,14 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
   ImplicitGroupLds<n, p>& I = Is[gp];
   Model md;
   md.load(theta);
+  // 1/theta_k, once per launch: the generated pieces and the Jacobian rows
+  // divide only by parameters, so the divisions become products with these
+  // wave-uniform reciprocals (scalar registers via readfirstlane)
+  float ith[p], jinv[4];
+#pragma unroll
+  for (int k = 0; k < p; ++k)
+    ith[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(1.0f / theta[k])));
+  jinv[0] = ith[3]; jinv[1] = ith[0]; jinv[2] = ith[1]; jinv[3] = ith[2];   // 1/mass, 1/Jx, 1/Jy, 1/Jz
   auto rec = [&](int t) { return ws + ((size_t)t * B + b) * W::REC; };
   auto active = [&](size_t tb, int a, float ua) -> bool {
     if (bd.mode == DILQR_BOUNDS_NONE) return false;
@@ -119,10 +127,10 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
       for (int i = 0; i < n; ++i) lam1[i] = I.vec[i];     // lam_{t+1} (0 at t = T-1)
       float Mc[d];
       if (t < T - 1) {
-        D2::mcol(r, theta, xt, ut, lam1, Mc);
+        D2::mcol(r, theta, ith, xt, ut, lam1, Mc);
         if (r < n) {
           float Fr[d];
-          md.template jac_row<false>(r, xt, ut, Fr);
+          md.jac_row_rcp(r, xt, ut, jinv, Fr);
 #pragma unroll
           for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
         }
@@ -202,7 +210,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         __syncthreads();
         if (r < n) {
           float Dr[d];
-          md.template jac_row<false>(r, xt, ut, Dr);
+          md.jac_row_rcp(r, xt, ut, jinv, Dr);
           float s = 0.f;
 #pragma unroll
           for (int j = 0; j < d; ++j) s += Dr[j] * I.vec[j];
@@ -258,7 +266,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
       // row r of D_t -> LDS (t = T-1: only for the carry's D_u, F_{T-1} is zero)
       if (r < n) {
         float Fr[d];
-        md.template jac_row<false>(r, xt, ut, Fr);
+        md.jac_row_rcp(r, xt, ut, jinv, Fr);
 #pragma unroll
         for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
       }
@@ -270,8 +278,8 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
           float lam1[n];
 #pragma unroll
           for (int i = 0; i < n; ++i) lam1[i] = I.lam[i];  // lam_{t+1}
-          D2::mcol(r, theta, xt, ut, lam1, Mc);
-          D2::mp_row(r, theta, xt, ut, lam1, Mp);
+          D2::mcol(r, theta, ith, xt, ut, lam1, Mc);
+          D2::mp_row(r, theta, ith, xt, ut, lam1, Mp);
         }
         __syncthreads();
         float z = 0.f;                                     // (M_t^T y_t)[r]
@@ -332,10 +340,10 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         if (r < n) {
           mu = hx - nd;
           float ft[p];
-          D2::xth_row(r, theta, xt, ut, ft);
+          D2::xth_row(r, theta, ith, xt, ut, ft);
 #pragma unroll
           for (int k = 0; k < p; ++k) acc[k] += ft[k] * mu;
-          D2::xx_row(r, theta, xt, ut, axr);
+          D2::xx_row(r, theta, ith, xt, ut, axr);
         }
 #pragma unroll
         for (int a = 0; a < m; ++a) au[a] = group_sum(r < n ? L.F[r][n + a] * mu : 0.f);

@@ -295,14 +295,28 @@ struct Rocket {
   // row r of get_linear_dyn (rocket.py:324-426), unclamped u.  RECIP: the
   // divisions by the mass and by J are products with reciprocals formed per
   // call (27 divisions over the 13 cases a 16-lane group executes -> 4); the
-  // implicit backward keeps the divisions (the reciprocals' live ranges cost
-  // its register-capped kernel more spills than the divisions cost, +7 %).
+  // F-from-HBM and forward paths keep the divisions.  jac_row_rcp: the
+  // reciprocals held by the caller (the implicit backward forms them once per
+  // launch, wave-uniform, in scalar registers).
   template <bool RECIP = true>
   DEV void jac_row(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M]) const {
+    if constexpr (RECIP) {
+      const float im = 1.f / mass;
+      jac_row_impl(r, x, u, D, [&](float v) { return v * im; },
+                   [&](float v, int k) { return v * (1.f / (k == 0 ? Jx : k == 1 ? Jy : Jz)); });
+    } else {
+      jac_row_impl(r, x, u, D, [&](float v) { return v / mass; },
+                   [&](float v, int k) { return v / (k == 0 ? Jx : k == 1 ? Jy : Jz); });
+    }
+  }
+  DEV void jac_row_rcp(int r, const float (&x)[N], const float (&u)[M], const float (&inv)[4],
+                       float (&D)[N + M]) const {
+    jac_row_impl(r, x, u, D, [&](float v) { return v * inv[0]; }, [&](float v, int k) { return v * inv[1 + k]; });
+  }
+  template <class BM, class BJ>
+  DEV void jac_row_impl(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M], BM by_mass,
+                        BJ byJ) const {
     const float dt = DT;
-    const float im = RECIP ? 1.f / mass : 1.f;
-    const auto by_mass = [&](float v) { return RECIP ? v * im : v / mass; };
-    const auto by = [](float v, float Jd, float ij) { return RECIP ? v * ij : v / Jd; };
     const float q0 = x[6], q1 = x[7], q2 = x[8], q3 = x[9], wx = x[10], wy = x[11], wz = x[12];
     const float ux = u[0], uy = u[1], uz = u[2];
 #pragma unroll
@@ -352,23 +366,17 @@ struct Rocket {
         D[6] = dt * 0.5f * wz; D[7] = dt * 0.5f * wy; D[8] = -dt * 0.5f * wx;
         D[10] = -dt * 0.5f * q2; D[11] = dt * 0.5f * q1; D[12] = dt * 0.5f * q0;
         break;
-      case 10: {
-        const float ij = RECIP ? 1.f / Jx : 1.f;
-        D[11] = by(-dt * (wz * Jz - wz * Jy), Jx, ij); D[12] = by(-dt * (wy * Jz - wy * Jy), Jx, ij);
+      case 10:
+        D[11] = byJ(-dt * (wz * Jz - wz * Jy), 0); D[12] = byJ(-dt * (wy * Jz - wy * Jy), 0);
         break;
-      }
-      case 11: {
-        const float ij = RECIP ? 1.f / Jy : 1.f;
-        D[10] = by(-dt * (wz * Jx - wz * Jz), Jy, ij); D[12] = by(-dt * (wx * Jx - wx * Jz), Jy, ij);
-        D[15] = by(dt * (l / 2), Jy, ij);
+      case 11:
+        D[10] = byJ(-dt * (wz * Jx - wz * Jz), 1); D[12] = byJ(-dt * (wx * Jx - wx * Jz), 1);
+        D[15] = byJ(dt * (l / 2), 1);
         break;
-      }
-      default: {  // 12
-        const float ij = RECIP ? 1.f / Jz : 1.f;
-        D[10] = by(-dt * (wy * Jy - wy * Jx), Jz, ij); D[11] = by(-dt * (wx * Jy - wx * Jx), Jz, ij);
-        D[14] = by(-dt * (l / 2), Jz, ij);
+      default:  // 12
+        D[10] = byJ(-dt * (wy * Jy - wy * Jx), 2); D[11] = byJ(-dt * (wx * Jy - wx * Jx), 2);
+        D[14] = byJ(-dt * (l / 2), 2);
         break;
-      }
     }
   }
 

@@ -60,19 +60,20 @@ WRAPM(Rocket, 13, 3)
 extern "C" void Rocket_pieces(const float* th, const float* x, const float* u, const float* lam, float* mcol,
                               float* mp, float* xx, float* xth) {
   using R = dilqr::gen::RocketD2;
-  float xx_[13], uu[3], ll[13];
+  float xx_[13], uu[3], ll[13], ith[5];
   for (int i = 0; i < 13; ++i) { xx_[i] = x[i]; ll[i] = lam[i]; }
   for (int i = 0; i < 3; ++i) uu[i] = u[i];
+  for (int k = 0; k < 5; ++k) ith[k] = 1.0f / th[k];
   for (int r = 0; r < 16; ++r) {
     float o16[16], o5[5], o13[13];
-    R::mcol(r, th, xx_, uu, ll, o16);
+    R::mcol(r, th, ith, xx_, uu, ll, o16);
     for (int k = 0; k < 16; ++k) mcol[r * 16 + k] = o16[k];
-    R::mp_row(r, th, xx_, uu, ll, o5);
+    R::mp_row(r, th, ith, xx_, uu, ll, o5);
     for (int k = 0; k < 5; ++k) mp[r * 5 + k] = o5[k];
     if (r < 13) {
-      R::xx_row(r, th, xx_, uu, o13);
+      R::xx_row(r, th, ith, xx_, uu, o13);
       for (int k = 0; k < 13; ++k) xx[r * 13 + k] = o13[k];
-      R::xth_row(r, th, xx_, uu, o5);
+      R::xth_row(r, th, ith, xx_, uu, o5);
       for (int k = 0; k < 5; ++k) xth[r * 5 + k] = o5[k];
     }
   }

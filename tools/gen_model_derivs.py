@@ -12,7 +12,7 @@ differ from the derivative (cartpole.py matrix_2_part_2/3 row 4).
 For the rocket (16 lanes per problem, dilqr_group.h) it emits per-lane pieces,
 built from the reference's build_batched_* tables (rocket.py:541-820) rather
 than from derivatives, since those are what its implicit backward uses:
-  mcol(r, ..., lam, o)   o[k] = sum_i lam_i Dtau[i][k][r]   (column r of M, d)
+  mcol(r, th, ith, ..., lam, o)   o[k] = sum_i lam_i Dtau[i][k][r]   (column r of M, d)
   mp_row(j, ..., lam, o) o[k] = sum_i lam_i D_params[i][j][k]                (p)
   xx_row(r, ..., o)      row r of x_grad_xtm1                                (n)
   xth_row(r, ..., o)     row r of x_grad_theta = d f_r / d theta             (p)
@@ -215,6 +215,19 @@ def rocket_block():
     sig = f"const float* __restrict__ th, const float (&x)[{n}], const float (&u)[{m}]"
     sig_l = sig + f", const float (&lam)[{n}]"
     up, upl = unpack_lines(xs, us, ps), unpack_lines(xs, us, ps, lam)
+    # the per-lane pieces of the implicit backward divide only by parameters
+    # (mass, inertias): the caller holds their reciprocals (ith[k] = 1/th[k],
+    # wave-uniform, formed once per launch), so a division becomes a product
+    ips = sp.symbols(f"ith0:{p}", real=True)
+
+    def rcp(e):
+        return sp.sympify(e).replace(lambda z: z.is_Pow and z.base in ps and z.exp.is_negative,
+                                     lambda z: ips[ps.index(z.base)] ** (-z.exp))
+    rc = lambda cases: {k: [rcp(e) for e in v] for k, v in cases.items()}  # noqa: E731
+    sig_r = f"const float* __restrict__ th, const float (&ith)[{p}], const float (&x)[{n}], const float (&u)[{m}]"
+    sig_rl = sig_r + f", const float (&lam)[{n}]"
+    iun = "\n    " + " ".join(f"[[maybe_unused]] const float {v} = ith[{i}];" for i, v in enumerate(ips))
+    upr, uplr = up + iun, upl + iun
     # get_matrices (rocket.py:258-261 with the build_batched_* tables)
     mats = [(f"Dp[{(i * d + j) * p + k}]", e) for (i, j, k), e in sorted(Dp.items())]
     mats += [(f"Dx[{(i * d + j) * n + k}]", e) for (i, j, k), e in sorted(Dx.items())]
@@ -224,10 +237,10 @@ def rocket_block():
     parts = ["struct RocketD2 {",
              f"  static constexpr int N = {n}, M = {m}, P = {p}, D = {d};",
              emit_ptr("matrices", sig + ", " + MAT_SIG, mats, up),
-             emit_switch("mcol", sig_l, "r", d, mcol, upl),
-             emit_switch("mp_row", sig_l, "j", p, mp, upl),
-             emit_switch("xx_row", sig, "r", n, xxr, up),
-             emit_switch("xth_row", sig, "r", p, xth, up),
+             emit_switch("mcol", sig_rl, "r", d, rc(mcol), uplr),
+             emit_switch("mp_row", sig_rl, "j", p, rc(mp), uplr),
+             emit_switch("xx_row", sig_r, "r", n, rc(xxr), upr),
+             emit_switch("xth_row", sig_r, "r", p, rc(xth), upr),
              "};"]
     return "\n".join(parts)
 

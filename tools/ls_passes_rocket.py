@@ -32,8 +32,14 @@ nb, _ = N.make_bounds(None, None)
 sv.begin(N.MODEL_ROCKET, theta, x0)
 for i in range(10):
     sv.iterate(N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, i, 1e-4, 0.0, 10 ** 9)
-    a = sv.alpha.view(-1, 4)
-    more = (a < 0.2 - 1e-7).float()
-    hist = {f"{x:g}": int((sv.alpha == x).sum()) for x in (1.0, 0.2, 0.04, 0.008, 0.0016)}
-    print(f"iter {i}: problems >1 pair pass {float(more.mean()):.3f}, waves {float(more.max(1).values.mean()):.3f}"
-          f"  alpha hist {hist}", flush=True)
+    al = sv.alpha
+    hist = {f"{x:g}": int((al == x).sum()) for x in (1.0, 0.2, 0.04, 0.008, 0.0016)}
+    # lane-pair search (today): 32 problems per wave, rounds of 2 candidates
+    w32 = al.view(-1, 32)
+    r2 = float((w32 < 0.2 - 1e-7).any(1).float().mean())          # some problem needs candidates 3+
+    r3 = float((w32 < 0.008 - 1e-9).any(1).float().mean())        # ... candidate 5
+    # a 4-lanes-per-problem search: 16 problems per wave, one round of 4 candidates
+    w16 = al.view(-1, 16)
+    q2 = float((w16 < 0.008 - 1e-9).any(1).float().mean())
+    print(f"iter {i}: alpha hist {hist}; 32-problem waves needing round 2 {r2:.3f}, round 3 {r3:.3f}; "
+          f"16-problem waves needing a 5th candidate {q2:.3f}", flush=True)
