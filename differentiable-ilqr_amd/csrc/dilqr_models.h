@@ -309,9 +309,24 @@ struct Rocket {
                    [&](float v, int k) { return v / (k == 0 ? Jx : k == 1 ? Jy : Jz); });
     }
   }
+  // Every row evaluated in every lane (compile-time rows: no divergence) and
+  // lane r keeping row r by selects — a switch on the lane's row makes the
+  // wave run all 13 cases behind exec-mask branches and merge the whole row
+  // after each (~24 register moves per case)
   DEV void jac_row_rcp(int r, const float (&x)[N], const float (&u)[M], const float (&inv)[4],
                        float (&D)[N + M]) const {
-    jac_row_impl(r, x, u, D, [&](float v) { return v * inv[0]; }, [&](float v, int k) { return v * inv[1 + k]; });
+    auto bm = [&](float v) { return v * inv[0]; };
+    auto bj = [&](float v, int k) { return v * inv[1 + k]; };
+#pragma unroll
+    for (int j = 0; j < N + M; ++j) D[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float Di[N + M];
+      jac_row_impl(i, x, u, Di, bm, bj);
+#pragma unroll
+      for (int j = 0; j < N + M; ++j)
+        if (j == i || FSparsity::nz(i, j)) D[j] = r == i ? Di[j] : D[j];
+    }
   }
   template <class BM, class BJ>
   DEV void jac_row_impl(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M], BM by_mass,
