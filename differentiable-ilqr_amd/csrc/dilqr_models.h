@@ -240,7 +240,15 @@ struct Rocket {
   static constexpr int N = 13, M = 3, P = 5;
   static constexpr float DT = 0.1f;
   float Jx, Jy, Jz, mass, l;
-  DEV void load(const float* __restrict__ th) { Jx = th[0]; Jy = th[1]; Jz = th[2]; mass = th[3]; l = th[4]; }
+  // 1/mass, 1/Jx, 1/Jy, 1/Jz: the same IEEE quotients deriv() and jac_row
+  // formed per call, formed once per launch (theta is the same for every
+  // problem: readfirstlane keeps them in scalar registers, no VGPRs)
+  float im, iJx, iJy, iJz;
+  DEV void load(const float* __restrict__ th) {
+    Jx = th[0]; Jy = th[1]; Jz = th[2]; mass = th[3]; l = th[4];
+    im = uniform(1.f / mass); iJx = uniform(1.f / Jx); iJy = uniform(1.f / Jy); iJz = uniform(1.f / Jz);
+  }
+  static DEV float uniform(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
   struct FSparsity {    // rocket.py:324-426 (69 nonzeros)
     static constexpr bool nz(int i, int j) {
@@ -260,7 +268,6 @@ struct Rocket {
   DEV float deriv(int r, const float (&x)[N], const float (&u)[M]) const {
 #pragma clang fp contract(off)
     const float q0 = x[6], q1 = x[7], q2 = x[8], q3 = x[9], wx = x[10], wy = x[11], wz = x[12];
-    const float im = 1.f / mass;
     const float Tx = fminf(fmaxf(u[0], -400.f), 400.f);
     const float Ty = fminf(fmaxf(u[1], -400.f), 400.f);
     const float Tz = fminf(fmaxf(u[2], -400.f), 400.f);
@@ -276,9 +283,9 @@ struct Rocket {
       case 7: return 0.5f * (((wx * q0) + (wz * q2)) + (-wy * q3));
       case 8: return 0.5f * (((wy * q0) + (-wz * q1)) + (wx * q3));
       case 9: return 0.5f * (((wz * q0) + (wy * q1)) + (-wx * q2));
-      case 10: return (1.f / Jx) * (0.f - (wy * (Jz * wz) - wz * (Jy * wy)));
-      case 11: return (1.f / Jy) * ((l / 2.f) * Tz - (wz * (Jx * wx) - wx * (Jz * wz)));
-      default: return (1.f / Jz) * (-(l / 2.f) * Ty - (wx * (Jy * wy) - wy * (Jx * wx)));
+      case 10: return iJx * (0.f - (wy * (Jz * wz) - wz * (Jy * wy)));
+      case 11: return iJy * ((l / 2.f) * Tz - (wz * (Jx * wx) - wx * (Jz * wz)));
+      default: return iJz * (-(l / 2.f) * Ty - (wx * (Jy * wy) - wy * (Jx * wx)));
     }
   }
 
@@ -301,9 +308,8 @@ struct Rocket {
   template <bool RECIP = true>
   DEV void jac_row(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M]) const {
     if constexpr (RECIP) {
-      const float im = 1.f / mass;
       jac_row_impl(r, x, u, D, [&](float v) { return v * im; },
-                   [&](float v, int k) { return v * (1.f / (k == 0 ? Jx : k == 1 ? Jy : Jz)); });
+                   [&](float v, int k) { return v * (k == 0 ? iJx : k == 1 ? iJy : iJz); });
     } else {
       jac_row_impl(r, x, u, D, [&](float v) { return v / mass; },
                    [&](float v, int k) { return v / (k == 0 ? Jx : k == 1 ? Jy : Jz); });
