@@ -585,7 +585,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    # under torchrun (RANK set) the process group is initialised even for one
+    # rank, so the RCCL path (init, barriers, the timing all-reduce) runs
+    # as it does at N > 1 (tests/test_dist.py drives it on one GPU)
+    dist = world > 1 or "RANK" in os.environ
     # BENCH_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one GPU
     # (the timing all-reduce then runs on the host); the driver's runs use RCCL
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")

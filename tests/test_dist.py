@@ -184,3 +184,26 @@ def test_bench_sharded_hip_path_equals_whole_batch(tmp_path):
         assert (lo, hi) == bench.shard_rows(B, world, rank)
         assert torch.equal(sh["u"], u[:, lo:hi].cpu()) and torch.equal(sh["x"], x[:, lo:hi].cpu())
         assert torch.equal(sh["cost"], cost[lo:hi].cpu())
+
+
+@pytest.mark.gpu
+def test_bench_rccl_path_runs(tmp_path):
+    """bench.py's RCCL branch — init_process_group("nccl"), the barriers around
+    the timed region and the max-over-ranks timing all-reduce on the device —
+    under torchrun with one rank on cuda:0 (one GPU per rank: a second rank
+    would need a second GPU), and its JSON line is well formed."""
+    import json
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--batch", "4096", "--steps", "3", "--warmup", "1", "--no-secondary", "--no-cpu-baseline"]
+    env = dict(os.environ)
+    env.pop("BENCH_DIST_BACKEND", None)
+    r = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0 and line["config"]["global_batch"] == 4096
