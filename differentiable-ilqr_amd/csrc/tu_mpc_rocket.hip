@@ -1,5 +1,6 @@
 // tu_mpc_rocket.hip — the fused iteration for the 16-lanes-per-problem model
 // (env_dx/rocket.py, n=13 m=3): standalone and device-resident MPC kernels.
+#include "dilqr_group8.h"
 #include "dilqr_lane_search.h"
 
 namespace dilqr {
@@ -70,22 +71,82 @@ __global__ void __launch_bounds__(64, DILQR_SWEEP_WAVES) k_mpc_sweep_group(int T
                            first ? S.Cpk : nullptr, first ? S.cost_sym : nullptr);
 }
 
+// The same sweep on 8 lanes per problem (dilqr_group8.h): 8 problems per wave,
+// the per-problem work (Jacobian, gain solve) repeated in 8 lanes instead of
+// 16.  Measured at config 3 (A/B on one box, tools/ab_rocket.py): MPC iteration
+// 0.400 -> 0.360 ms, the steady sweep 255 -> 197 us.
+#ifndef DILQR_SWEEP8_WAVES
+#define DILQR_SWEEP8_WAVES 3
+#endif
+template <class Model, int MODE, bool DCONST>
+__global__ void __launch_bounds__(64, DILQR_SWEEP8_WAVES) k_mpc_sweep_g8(int T, int B, const float* __restrict__ theta,
+                                                                         const float* __restrict__ C,
+                                                                         const float* __restrict__ c, Bounds bd,
+                                                                         int iteration, float eps, int not_improved_lim,
+                                                                         int G, MpcState S) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  __shared__ Group8Lds<n, m> Ls[kG8PW];
+  if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
+  const bool first = iteration == 0;
+  const int l = threadIdx.x & (kG8 - 1), gp = threadIdx.x / kG8;
+  const int b0 = blockIdx.x * kG8PW + gp;
+  const bool valid = b0 < B;
+  const int b = valid ? b0 : B - 1;
+  Model md; md.load(theta);
+  const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
+  const int cur = S.slot[b];
+  // the register cost when every problem of the wave has one (wave-uniform);
+  // the two kinds of wave run in two instantiations launched back to back,
+  // each leaving the other's waves at once
+  const bool dconst = !first && S.Cpk && S.cost_sym[b] == 7;
+  if (__all(dconst) != DCONST) return;
+  Group8Cost cs{C, c, DCONST, {0.f, 0.f}, {0.f, 0.f}};
+  if (DCONST) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      cs.cd[k] = S.Cpk[(size_t)b * 2 * d + l + kG8 * k];        // rows l, l + 8
+      cs.cc[k] = S.Cpk[(size_t)b * 2 * d + d + l + kG8 * k];
+    }
+  }
+  group8_sweep<Model, MODE, DCONST>(Ls[gp], T, B, b, l, valid, md, cs, S.Xs + cur * TBn, S.Us + cur * TBm, bd, S.ws,
+                            first ? S.Cpk : nullptr, first ? S.cost_sym : nullptr);
+}
+
+// DILQR_SWEEP_LANES: 8 (default) or 16 lanes per problem in the MPC sweep (the
+// 16-lane kernel stays for A/B builds)
+#ifndef DILQR_SWEEP_LANES
+#define DILQR_SWEEP_LANES 8
+#endif
 int launch_mpc_step_rocket(const MpcStepArgs& a) {
 #define SEARCH(BM_, DC_)                                                                                          \
   k_mpc_search_lane<Rocket, BM_, DC_><<<grid_for(2 * (long long)a.B), kBlock, 0, a.stream>>>(                     \
       a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st)
+#if DILQR_SWEEP_LANES == 8
+#define SWEEP8(MODE_, DC_)                                                                                        \
+  k_mpc_sweep_g8<Rocket, MODE_, DC_><<<(int)((a.B + kG8PW - 1) / kG8PW), 64, 0, a.stream>>>(                     \
+      a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st)
+#define SWEEP(MODE_)                                                                                              \
+  SWEEP8(MODE_, true);                                                                                            \
+  SWEEP8(MODE_, false)
+#else
+#define SWEEP(MODE_)                                                                                              \
+  k_mpc_sweep_group<Rocket, MODE_><<<grid_group(a.B), 64, 0, a.stream>>>(                                         \
+      a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st)
+#endif
   if (a.bd.mode != DILQR_BOUNDS_NONE) {
-    k_mpc_sweep_group<Rocket, GAIN_BOX><<<grid_group(a.B), 64, 0, a.stream>>>(
-        a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st);
+    SWEEP(GAIN_BOX);
     SEARCH(DILQR_BOUNDS_SCALAR, true);
     SEARCH(DILQR_BOUNDS_SCALAR, false);
   } else {
-    k_mpc_sweep_group<Rocket, GAIN_UNC><<<grid_group(a.B), 64, 0, a.stream>>>(
-        a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st);
+    SWEEP(GAIN_UNC);
     SEARCH(DILQR_BOUNDS_NONE, true);
     SEARCH(DILQR_BOUNDS_NONE, false);
   }
 #undef SEARCH
+#undef SWEEP
+#if DILQR_SWEEP_LANES == 8
+#undef SWEEP8
+#endif
   return launched();
 }
 
