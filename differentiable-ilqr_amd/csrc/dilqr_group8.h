@@ -55,10 +55,14 @@ struct Group8Lds {
     float Q[d][QS];
   };
   float Kk[m][W];                                // gains K (box mode: every lane needs all of K)
+  // The 4 problems of a half-wave (a b32 read's lane group) read the same
+  // relative words; struct strides of 8 mod 16 words put them on 4 disjoint
+  // 8-bank sets (16 mod 32 paired them: a 2-way conflict on every column read,
+  // 40 % of the sweep's LDS cycles in SQ_LDS_BANK_CONFLICT)
   static constexpr int kWords = d * QS + m * W;
-  float pad[((16 - kWords % 32) % 32 + 32) % 32];
+  float pad[(8 - kWords % 16 + 16) % 16];
 };
-static_assert(sizeof(Group8Lds<13, 3>) / 4 % 32 == 16, "bank offset between problems");
+static_assert(sizeof(Group8Lds<13, 3>) / 4 % 16 == 8, "bank offset between problems");
 
 // Two right-hand sides of group_gains_col at once (columns ja, jb of the gain
 // matrix; j = n is k): the same elimination, each column's own substitution.
