@@ -62,14 +62,14 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
   ImplicitGroupLds<n, p>& I = Is[gp];
   Model md;
   md.load(theta);
-  // 1/theta_k, once per launch: the generated pieces and the Jacobian rows
-  // divide only by parameters, so the divisions become products with these
-  // wave-uniform reciprocals (scalar registers via readfirstlane)
-  float ith[p], jinv[4];
+  // 1/theta_k, once per launch: the generated pieces divide only by
+  // parameters, so the divisions become products with these wave-uniform
+  // reciprocals (scalar registers via readfirstlane); the Jacobian rows take
+  // the model's per-launch coefficients (Rocket::load)
+  float ith[p];
 #pragma unroll
   for (int k = 0; k < p; ++k)
     ith[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(1.0f / theta[k])));
-  jinv[0] = ith[3]; jinv[1] = ith[0]; jinv[2] = ith[1]; jinv[3] = ith[2];   // 1/mass, 1/Jx, 1/Jy, 1/Jz
   auto rec = [&](int t) { return ws + ((size_t)t * B + b) * W::REC; };
   auto active = [&](size_t tb, int a, float ua) -> bool {
     if (bd.mode == DILQR_BOUNDS_NONE) return false;
@@ -130,7 +130,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         D2::mcol(r, theta, ith, xt, ut, lam1, Mc);
         if (r < n) {
           float Fr[d];
-          md.jac_row_rcp(r, xt, ut, jinv, Fr);
+          md.jac_row_sel(r, xt, ut, Fr);
 #pragma unroll
           for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
         }
@@ -210,7 +210,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         __syncthreads();
         if (r < n) {
           float Dr[d];
-          md.jac_row_rcp(r, xt, ut, jinv, Dr);
+          md.jac_row_sel(r, xt, ut, Dr);
           float s = 0.f;
 #pragma unroll
           for (int j = 0; j < d; ++j) s += Dr[j] * I.vec[j];
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
       // row r of D_t -> LDS (t = T-1: only for the carry's D_u, F_{T-1} is zero)
       if (r < n) {
         float Fr[d];
-        md.jac_row_rcp(r, xt, ut, jinv, Fr);
+        md.jac_row_sel(r, xt, ut, Fr);
 #pragma unroll
         for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
       }

@@ -244,9 +244,19 @@ struct Rocket {
   // formed per call, formed once per launch (theta is the same for every
   // problem: readfirstlane keeps them in scalar registers, no VGPRs)
   float im, iJx, iJy, iJz;
+  // jac_row's coefficients, per launch (scalar registers): dt/m, 2 dt/m, and
+  // the angular rows' -dt (J_j - J_k)/J_i and +-dt (l/2)/J_i
+  float s1, s2, w10, w11, w12, l11, l12;
   DEV void load(const float* __restrict__ th) {
     Jx = th[0]; Jy = th[1]; Jz = th[2]; mass = th[3]; l = th[4];
     im = uniform(1.f / mass); iJx = uniform(1.f / Jx); iJy = uniform(1.f / Jy); iJz = uniform(1.f / Jz);
+    s1 = uniform(DT * im);
+    s2 = uniform(2.f * s1);
+    w10 = uniform((-DT * (Jz - Jy)) * iJx);
+    w11 = uniform((-DT * (Jx - Jz)) * iJy);
+    w12 = uniform((-DT * (Jy - Jx)) * iJz);
+    l11 = uniform((DT * (l / 2.f)) * iJy);
+    l12 = uniform((-DT * (l / 2.f)) * iJz);
   }
   static DEV float uniform(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
@@ -299,77 +309,49 @@ struct Rocket {
 #pragma clang fp contract(off)
     return x[r] + deriv(r, x, u) * DT;
   }
-  // row r of get_linear_dyn (rocket.py:324-426), unclamped u.  RECIP: the
-  // divisions by the mass and by J are products with reciprocals formed per
-  // call (27 divisions over the 13 cases a 16-lane group executes -> 4); the
-  // F-from-HBM and forward paths keep the divisions.  jac_row_rcp: the
-  // reciprocals held by the caller (the implicit backward forms them once per
-  // launch, wave-uniform, in scalar registers).
-  template <bool RECIP = true>
+  // row r of get_linear_dyn (rocket.py:324-426), unclamped u, factored over
+  // the per-launch coefficients of load(): rows 3-5 are 2 dt/m times the
+  // derivative of R(q) T (d/dq: bilinear in q and T; d/dT: R(q)), rows 6-9
+  // +-dt/2 times w or q, rows 10-12 a coefficient times one rate (27 divisions
+  // and ~50 products per Jacobian in the reference's order become ~15
+  // products: the 16- and 8-lane kernels evaluate the whole Jacobian in every
+  // lane).  The same real numbers as the reference's expressions, rounded in
+  // another order (parity at 1e-4 against the float64 oracle).
   DEV void jac_row(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M]) const {
-    if constexpr (RECIP) {
-      jac_row_impl(r, x, u, D, [&](float v) { return v * im; },
-                   [&](float v, int k) { return v * (k == 0 ? iJx : k == 1 ? iJy : iJz); });
-    } else {
-      jac_row_impl(r, x, u, D, [&](float v) { return v / mass; },
-                   [&](float v, int k) { return v / (k == 0 ? Jx : k == 1 ? Jy : Jz); });
-    }
-  }
-  // Every row evaluated in every lane (compile-time rows: no divergence) and
-  // lane r keeping row r by selects — a switch on the lane's row makes the
-  // wave run all 13 cases behind exec-mask branches and merge the whole row
-  // after each (~24 register moves per case)
-  DEV void jac_row_rcp(int r, const float (&x)[N], const float (&u)[M], const float (&inv)[4],
-                       float (&D)[N + M]) const {
-    auto bm = [&](float v) { return v * inv[0]; };
-    auto bj = [&](float v, int k) { return v * inv[1 + k]; };
-#pragma unroll
-    for (int j = 0; j < N + M; ++j) D[j] = 0.f;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      float Di[N + M];
-      jac_row_impl(i, x, u, Di, bm, bj);
-#pragma unroll
-      for (int j = 0; j < N + M; ++j)
-        if (j == i || FSparsity::nz(i, j)) D[j] = r == i ? Di[j] : D[j];
-    }
-  }
-  template <class BM, class BJ>
-  DEV void jac_row_impl(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M], BM by_mass,
-                        BJ byJ) const {
     const float dt = DT;
     const float q0 = x[6], q1 = x[7], q2 = x[8], q3 = x[9], wx = x[10], wy = x[11], wz = x[12];
     const float ux = u[0], uy = u[1], uz = u[2];
+    const float a = s2;
 #pragma unroll
     for (int j = 0; j < N + M; ++j) D[j] = (j == r) ? 1.f : 0.f;
     switch (r) {
       case 0: case 1: case 2: D[r + 3] = dt; break;
       case 3:
-        D[6] = by_mass(dt * (uz * 2 * q2 - uy * 2 * q3));
-        D[7] = by_mass(dt * (uy * 2 * q2 + uz * 2 * q3));
-        D[8] = by_mass(dt * (uy * 2 * q1 - ux * 4 * q2 + uz * 2 * q0));
-        D[9] = by_mass(dt * (uz * 2 * q1 - ux * 4 * q3 - uy * 2 * q0));
-        D[13] = by_mass(dt * (1 - 2 * (q2 * q2 + q3 * q3)));
-        D[14] = by_mass(dt * 2 * (q1 * q2 - q0 * q3));
-        D[15] = by_mass(dt * 2 * (q1 * q3 + q0 * q2));
+        D[6] = a * (uz * q2 - uy * q3);
+        D[7] = a * (uy * q2 + uz * q3);
+        D[8] = a * ((uy * q1 - 2.f * ux * q2) + uz * q0);
+        D[9] = a * ((uz * q1 - 2.f * ux * q3) - uy * q0);
+        D[13] = s1 - a * (q2 * q2 + q3 * q3);
+        D[14] = a * (q1 * q2 - q0 * q3);
+        D[15] = a * (q1 * q3 + q0 * q2);
         break;
       case 4:
-        D[6] = by_mass(dt * (ux * 2 * q3 - uz * 2 * q1));
-        D[7] = by_mass(dt * (ux * 2 * q2 - uy * 4 * q1 - uz * 2 * q0));
-        D[8] = by_mass(dt * (ux * 2 * q1 + uz * 2 * q3));
-        D[9] = by_mass(dt * (ux * 2 * q0 - uy * 4 * q3 + uz * 2 * q2));
-        D[13] = by_mass(dt * 2 * (q1 * q2 + q0 * q3));
-        D[14] = by_mass(dt * (1 - 2 * (q1 * q1 + q3 * q3)));
-        D[15] = by_mass(dt * 2 * (q2 * q3 - q0 * q1));
+        D[6] = a * (ux * q3 - uz * q1);
+        D[7] = a * ((ux * q2 - 2.f * uy * q1) - uz * q0);
+        D[8] = a * (ux * q1 + uz * q3);
+        D[9] = a * ((ux * q0 - 2.f * uy * q3) + uz * q2);
+        D[13] = a * (q1 * q2 + q0 * q3);
+        D[14] = s1 - a * (q1 * q1 + q3 * q3);
+        D[15] = a * (q2 * q3 - q0 * q1);
         break;
       case 5:
-        D[6] = by_mass(dt * (uy * 2 * q1 - ux * 2 * q2));
-        D[7] = by_mass(dt * (ux * 2 * q3 + uy * 2 * q0 - uz * 4 * q1));
-        D[8] = by_mass(dt * (uy * 2 * q3 - ux * 2 * q0 - uz * 4 * q2));
-        D[9] = by_mass(dt * (ux * 2 * q1 + uy * 2 * q2));
-        D[13] = by_mass(dt * 2 * (q1 * q3 - q0 * q2));
-        D[14] = by_mass(dt * 2 * (q2 * q3 + q0 * q1));
-        D[15] = by_mass(dt * (1 - 2 * (q1 * q1 + q2 * q2)));
+        D[6] = a * (uy * q1 - ux * q2);
+        D[7] = a * ((ux * q3 + uy * q0) - 2.f * uz * q1);
+        D[8] = a * ((uy * q3 - ux * q0) - 2.f * uz * q2);
+        D[9] = a * (ux * q1 + uy * q2);
+        D[13] = a * (q1 * q3 - q0 * q2);
+        D[14] = a * (q2 * q3 + q0 * q1);
+        D[15] = s1 - a * (q1 * q1 + q2 * q2);
         break;
       case 6:
         D[7] = -dt * 0.5f * wx; D[8] = -dt * 0.5f * wy; D[9] = -dt * 0.5f * wz;
@@ -387,17 +369,25 @@ struct Rocket {
         D[6] = dt * 0.5f * wz; D[7] = dt * 0.5f * wy; D[8] = -dt * 0.5f * wx;
         D[10] = -dt * 0.5f * q2; D[11] = dt * 0.5f * q1; D[12] = dt * 0.5f * q0;
         break;
-      case 10:
-        D[11] = byJ(-dt * (wz * Jz - wz * Jy), 0); D[12] = byJ(-dt * (wy * Jz - wy * Jy), 0);
-        break;
-      case 11:
-        D[10] = byJ(-dt * (wz * Jx - wz * Jz), 1); D[12] = byJ(-dt * (wx * Jx - wx * Jz), 1);
-        D[15] = byJ(dt * (l / 2), 1);
-        break;
-      default:  // 12
-        D[10] = byJ(-dt * (wy * Jy - wy * Jx), 2); D[11] = byJ(-dt * (wx * Jy - wx * Jx), 2);
-        D[14] = byJ(-dt * (l / 2), 2);
-        break;
+      case 10: D[11] = w10 * wz; D[12] = w10 * wy; break;
+      case 11: D[10] = w11 * wz; D[12] = w11 * wx; D[15] = l11; break;
+      default: D[10] = w12 * wy; D[11] = w12 * wx; D[14] = l12; break;   // 12
+    }
+  }
+  // Every row evaluated in every lane (compile-time rows: no divergence) and
+  // lane r keeping row r by selects — a switch on the lane's row makes the
+  // wave run all 13 cases behind exec-mask branches and merge the whole row
+  // after each (~24 register moves per case)
+  DEV void jac_row_sel(int r, const float (&x)[N], const float (&u)[M], float (&D)[N + M]) const {
+#pragma unroll
+    for (int j = 0; j < N + M; ++j) D[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float Di[N + M];
+      jac_row(i, x, u, Di);
+#pragma unroll
+      for (int j = 0; j < N + M; ++j)
+        if (j == i || FSparsity::nz(i, j)) D[j] = r == i ? Di[j] : D[j];
     }
   }
 
