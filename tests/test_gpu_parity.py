@@ -930,6 +930,24 @@ def test_rocket_fused_iteration_equals_unfused(golden):
         assert same_bits(ta, tb), relerr(cpu(ta), cpu(tb))
 
 
+@pytest.mark.parametrize("bounds", [(-10.0, 10.0), (-3.0, 3.0)])
+def test_rocket_fused_iteration_equals_unfused_box(golden, bounds):
+    """The bounded rocket MPC: the 8-lane sweep's box mode (pnqp once per lane,
+    two gain columns per lane, the V columns from all of K) against the unfused
+    16-lane kernels with F in HBM, bit for bit, and the box actually active."""
+    g = golden("mpc_f64")
+    mname, T, it, _b, eps, nil, decay, mls = MPC_CASES["rocket_unc"]
+    x0 = g["rocket_unc_x0"]
+    a = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls, fused=True)
+    b = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls, fused=False)
+    for ta, tb in zip(a, b):
+        assert same_bits(ta, tb), relerr(cpu(ta), cpu(tb))
+    u = cpu(a[1])
+    at_bound = np.isclose(np.abs(u), bounds[1]).mean()
+    print(f"\n[rocket box {bounds}] controls at a bound: {at_bound:.2f}")
+    assert at_bound > 0.0 and np.abs(u).max() <= bounds[1]
+
+
 def test_rocket_mpc_full_size_batch_independence():
     """Config 3 shape (B=32768, T=30): a solve over the whole batch returns, for
     a sample of problems, what solving those problems alone returns."""
