@@ -88,6 +88,9 @@ DEV float lane_stage_cost(const float (&tau)[d], const float (&cd)[d], const flo
 // DCONST: the whole wave's problems hold a time-invariant diagonal cost in
 // registers (cd, cc), else every lane reads the caller's rows (a flagged
 // problem's rows hold the same values).  Writes x/u to (xo, uo) when `wr`.
+#ifndef DILQR_SEARCH_PFD
+#define DILQR_SEARCH_PFD 1
+#endif
 template <class Model, int BM, bool DCONST>
 DEV void lane_pass(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
                    const float (&cd)[Model::N + Model::M], const float (&cc)[Model::N + Model::M],
@@ -142,16 +145,24 @@ DEV void lane_pass(int T, int B, int b, const Model& md, const float* __restrict
       if (wr) st(xo + (tb + B) * n, xs);
     }
   };
-  // two input buffers in ping-pong (step t+1's loads in flight while step t
-  // computes; no copies between them)
-  LaneIn<n, m, GREC> b0, b1;
-  b0.load(ws, x, u, 0, B, b);
-  for (int t = 0; t < T; t += 2) {
-    if (t + 1 < T) b1.load(ws, x, u, t + 1, B, b);
-    body(t, b0);
-    if (t + 1 < T) {
-      if (t + 2 < T) b0.load(ws, x, u, t + 2, B, b);
-      body(t + 1, b1);
+  // a ring of PFD + 1 input buffers: step t+PFD's loads in flight while step
+  // t computes (the loop unrolled PFD + 1 times, so the buffers rotate by
+  // name, no copies).  Measured at config 3 (tools/ab_rocket.py, one box):
+  // PFD 1 0.339-0.351 ms per MPC iteration, 2 0.356-0.368, 3 0.358-0.364 —
+  // a search round streams ~360 MB (gain records, the current trajectory, two
+  // candidates out) at ~5 TB/s, so deeper prefetch only adds registers.
+  constexpr int P = DILQR_SEARCH_PFD + 1;
+  LaneIn<n, m, GREC> ring[P];
+#pragma unroll
+  for (int i = 0; i < P - 1; ++i)
+    if (i < T) ring[i].load(ws, x, u, i, B, b);
+  for (int t = 0; t < T; t += P) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      if (t + j < T) {
+        if (t + j + P - 1 < T) ring[(j + P - 1) % P].load(ws, x, u, t + j + P - 1, B, b);
+        body(t + j, ring[j]);
+      }
     }
   }
   cost = sc;
