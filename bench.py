@@ -383,7 +383,7 @@ def secondary_configs(dev):
     nb, _ = N.make_bounds(None, None)
     val, ms_it = _timed_solves(sv, N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, 10, 2, 1)
     # the launches the timed solves run per iteration, steady state: the group
-    # sweep (16 lanes per problem) and the line search (one problem per lane)
+    # sweep (8 lanes per problem) and the line search (one candidate per lane)
     it_ms = steady_iteration_ms(ops.MPCSolve(T, B, n, m, dev), N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, dev)
     d = n + m
     # bytes of one steady iteration as the kernels move them (counted the way
@@ -399,9 +399,9 @@ def secondary_configs(dev):
     out["config3_rocket"] = {
         "value": val, "unit": "problem-iters/s", "ms_per_iter": ms_it, "batch": B, "T": T,
         "fused_iteration": with_pmc(
-            {"kernel": "k_mpc_sweep_group<Rocket,UNC> + k_mpc_search_lane<Rocket,NONE,register cost> (+ the "
-                       "dense-cost instantiation, which leaves at once): one MPC iteration of the timed solves, "
-                       "steady state",
+            {"kernel": "k_mpc_sweep_g8<Rocket,UNC,register cost> + k_mpc_search_lane<Rocket,NONE,register cost> "
+                       "(+ the dense-cost instantiations, which leave at once): one MPC iteration of the timed "
+                       "solves, steady state",
              "bound": "hbm", "avg_launch_ms": it_ms, "algorithmic_bytes_per_launch": it_bytes,
              "bytes_model": "cost as read (time-invariant diagonal: 2d floats in registers) + x_init + tau in/out "
                             "+ cost, du_norm + gain records through HBM (2 T (mn+m) floats)",
@@ -409,8 +409,8 @@ def secondary_configs(dev):
              "survey_bytes_note": "SURVEY.md §8(d) 36,540 B/problem counts the caller's C at every step, which the "
                                   "steady kernels never read (not a roofline figure)",
              "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
-            ("k_mpc_sweep_group<Rocket, 0>", "k_mpc_search_lane<Rocket, 0, true>",
-             "k_mpc_search_lane<Rocket, 0, false>")),
+            ("k_mpc_sweep_g8<Rocket, 0, true>", "k_mpc_sweep_g8<Rocket, 0, false>",
+             "k_mpc_search_lane<Rocket, 0, true>", "k_mpc_search_lane<Rocket, 0, false>")),
         "riccati_sweep": sweep_roofline(n, m, T, B, dev)}
     # rocket implicit backward (16-lane groups) at the solution of the timed solves
     x, u = sv.gather_best()
@@ -511,7 +511,7 @@ def profile_set(name, dev):
     from dilqr import ops
     from dilqr.implicit import implicit_backward
     out = {}
-    if name == "rocket":                          # k_mpc_sweep_group + k_mpc_search_lane<Rocket>, config 3
+    if name == "rocket":                          # k_mpc_sweep_g8 + k_mpc_search_lane<Rocket>, config 3
         T, B = 30, 32768
         dx, x0, C, c = rocket_problems(B, dev)
         theta = ops.theta_of(dx, x0)
