@@ -61,8 +61,8 @@ class F32Printer(C99CodePrinter):
         return f"powf({self._print(b)}, {self._print(ex)})"
 
     def _print_Function(self, e):
-        name = {"sin": "sinf", "cos": "cosf", "atan2": "atan2f", "sqrt": "sqrtf", "exp": "expf"}.get(
-            e.func.__name__)
+        name = {"sin": "sinf", "cos": "cosf", "atan2": "atan2f", "sqrt": "sqrtf", "exp": "expf",
+                "vrcp": "vrcp"}.get(e.func.__name__)
         if name:
             return f"{name}({', '.join(self._print(a) for a in e.args)})"
         return super()._print_Function(e)
@@ -78,10 +78,27 @@ def _f32_calls(txt):
     return txt
 
 
+VRCP = sp.Function("vrcp")
+
+
+def hw_rcp(e):
+    """Every division by a state-dependent (or parameter) expression as the
+    hardware reciprocal, 1/b^k -> vrcp(b^k) (v_rcp_f32, 1 ulp; an IEEE f32
+    division is ~10 instructions on gfx950), so the C printer emits no `/`
+    but constant rationals."""
+    return sp.sympify(e).replace(lambda z: z.is_Pow and z.exp.is_Integer and z.exp < 0,
+                                 lambda z: VRCP(z.base ** (-z.exp)))
+
+
+def cse_rcp(exprs):
+    repl, red = sp.cse(exprs, symbols=sp.numbered_symbols("s"), optimizations="basic")
+    return [(v, hw_rcp(e)) for v, e in repl], [hw_rcp(e) for e in red]
+
+
 def emit(name, args_sig, outputs, out_decl, syms):
     """outputs: list of (lvalue string, expr)."""
     exprs = [e for _, e in outputs]
-    repl, red = sp.cse(exprs, symbols=sp.numbered_symbols("s"), optimizations="basic")
+    repl, red = cse_rcp(exprs)
     lines = [f"  static DEV void {name}({args_sig}, {out_decl}) {{"]
     lines += [f"    const float {s[0]} = {P.doprint(s[1])};" for s in repl]
     for (lv, _), e in zip(outputs, red):
@@ -103,7 +120,7 @@ def emit_ptr(name, sig, outputs, unpack):
     """A function writing the nonzero entries `outputs` [(lvalue, expr)] through
     pointers (get_matrices; the caller zero-fills the rest), CSE'd."""
     nz = [(lv, e) for lv, e in outputs if e != 0]
-    repl, red = sp.cse([e for _, e in nz], symbols=sp.numbered_symbols("s"), optimizations="basic")
+    repl, red = cse_rcp([e for _, e in nz])
     lines = [f"  static DEV void {name}({sig}) {{", unpack]
     lines += [f"    const float {v} = {P.doprint(e)};" for v, e in repl]
     lines += [f"    {lv} = {P.doprint(e)};" for (lv, _), e in zip(nz, red)]
@@ -183,7 +200,7 @@ def emit_switch(name, sig, sel, n_out, cases, unpack):
         nz = [(k, e) for k, e in enumerate(exprs) if e != 0]
         if not nz:
             continue
-        repl, red = sp.cse([e for _, e in nz], symbols=sp.numbered_symbols("s"), optimizations="basic")
+        repl, red = cse_rcp([e for _, e in nz])
         lines.append(f"      case {val}: {{")
         lines += [f"        const float {v} = {P.doprint(e)};" for v, e in repl]
         lines += [f"        o[{k}] = {P.doprint(e)};" for (k, _), e in zip(nz, red)]
@@ -199,7 +216,7 @@ def emit_select(name, sig, sel, n_out, cases, unpack):
     every case anyway, each behind an exec-mask branch, and merge the whole
     output array after each case (measured: ~24 register moves per case)."""
     items = [(val, k, e) for val in sorted(cases) for k, e in enumerate(cases[val]) if e != 0]
-    repl, red = sp.cse([e for _, _, e in items], symbols=sp.numbered_symbols("s"), optimizations="basic")
+    repl, red = cse_rcp([e for _, _, e in items])
     lines = [f"  static DEV void {name}(int {sel}, {sig}, float (&o)[{n_out}]) {{", unpack,
              f"#pragma unroll\n    for (int k = 0; k < {n_out}; ++k) o[k] = 0.f;"]
     lines += [f"    const float {v} = {P.doprint(e)};" for v, e in repl]
@@ -272,6 +289,7 @@ def main():
            "#else  // host build (tests/test_models_gen.py compiles this header with g++)",
            "#include <cmath>",
            "#define DEV inline",
+           "inline float vrcp(float x) { return 1.0f / x; }",
            "#endif", "", "namespace dilqr {", "namespace gen {", ""]
     src = "\n".join(hdr) + "\n\n".join(blocks) + "\n\n}  // namespace gen\n}  // namespace dilqr\n"
     with open(OUT, "w") as fh:
