@@ -54,16 +54,24 @@ template <int n, int m>
 struct GroupLds {
   static constexpr int d = n + m;
   static constexpr int W = 16;                 // padded row width (b128 reads)
-  float V[n][W];
+  // V and F rows 20 words apart: a lane's 16-byte row stores then start on 8
+  // distinct 4-bank sets across the 8 lanes of a store group (a 16-word stride
+  // put 4 lanes on each of 2 sets: 26 % of the implicit backward's LDS cycles
+  // were bank conflicts)
+#ifndef DILQR_GROUP_RS
+#define DILQR_GROUP_RS 20
+#endif
+  static constexpr int RS = DILQR_GROUP_RS;
+  float V[n][RS];
   float v[W];
-  float F[n][W];
+  float F[n][RS];
   float Qu[m][W + 4];                          // u rows of Q, q_u at [.][W]
   float Kk[m][W + 4];                          // gains K, k at [.][W]
   float tau[W];
   // tau2: the paired line search's second candidate; its tail pads the struct
   // to 16 words mod 32, so the two groups of a half-wave read columns from
   // disjoint LDS banks (see GroupLdsT)
-  static constexpr int kWords = 2 * n * W + W + 2 * m * (W + 4) + 2 * W;
+  static constexpr int kWords = 2 * n * RS + W + 2 * m * (W + 4) + 2 * W;
   float tau2[W + ((16 - kWords % 32) % 32 + 32) % 32];
 };
 

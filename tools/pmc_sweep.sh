@@ -1,7 +1,8 @@
 #!/usr/bin/env bash
 # LDS / issue counters of one kernel family (PSET, default rocket) for the
 # in-tree library and every ab/libdilqr_<V>.so variant: one counter group per
-# pass, kernel trace only.  Output: gpurun_out/pmcs/<variant>_p<i>/.
+# pass, kernel trace only (PMCS_VARIANTS=0: the in-tree library only).
+# Output: gpurun_out/pmcs/<variant>_p<i>/.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT=$R/gpurun_out/pmcs
@@ -15,7 +16,9 @@ GROUPS_=("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY"
          "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_DATA_FIFO_FULL"
          "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_CMD_FIFO_FULL SQ_LDS_UNALIGNED_STALL"
          "SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_INST_LEVEL_LDS")
-for f in $OUT/.inplace.so $R/ab/libdilqr_*.so; do
+VARIANTS=$R/ab/libdilqr_*.so
+[ "${PMCS_VARIANTS:-1}" = "0" ] && VARIANTS=
+for f in $OUT/.inplace.so $VARIANTS; do
   [ -f "$f" ] || continue
   v=$(basename $f .so); v=${v#libdilqr_}; [ "$v" = ".inplace" ] && v=inplace
   cp $f $L
