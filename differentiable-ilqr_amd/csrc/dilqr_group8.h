@@ -17,9 +17,8 @@
 // each half of the rows, then the two halves), so this sweep and
 // k_lqr_backward_group agree exactly (test_rocket_fused_vs_unfused).
 //
-// LDS banks: lane l stores rows l and l+8 as 16-byte pieces at a row stride of
-// 20 words, so the 8 lanes of a problem start 20 words apart — 8 disjoint
-// 4-bank sets (rows 2l, 2l+1 at stride 16 put all 8 lanes on the same 4 banks).
+// LDS banks: lane l stores rows l and l+8 at a row stride of 17 words (see
+// Group8Lds; rows 2l, 2l+1 at stride 16 put all 8 lanes on the same banks).
 #pragma once
 #include "dilqr_fused.h"
 #include "dilqr_group.h"
@@ -42,27 +41,37 @@ DEV float group8_sum(float pa, float pb) {
   return pa + pb;
 }
 
-template <int n, int m>
+// Q / W row stride 17 (odd): 4-byte stores, but a problem's block is 280
+// words instead of 376, so 4 workgroups (waves) per SIMD fit the LDS and the
+// register-cost kernel's 121 VGPRs — 4 096 waves in one round instead of 1.33
+// rounds at 3 per SIMD.  Bank-conflict-free: lane l's row starts 17 l words
+// in, blocks 8 mod 16 words apart.  Measured at config 3 (A/B on one box,
+// 3 rounds): MPC iteration 0.345-0.352 -> 0.321-0.327 ms against stride 20.
+#ifndef DILQR_G8_QS
+#define DILQR_G8_QS 17
+#endif
+template <int n, int m, bool KK = true>
 struct Group8Lds {
   static constexpr int d = n + m;
   static constexpr int W = 16;
-  static constexpr int QS = W + 4;               // Q row stride: 16-byte aligned rows, q_r at [d]
+  static constexpr int QS = DILQR_G8_QS;         // Q row stride, q_r at [d]
   // W^T rows and Q share the words: a workgroup is one wave, whose LDS
   // accesses complete in program order, so Q's stores (after every lane's
-  // W column reads) cannot overtake them.  Smaller blocks: 3 workgroups per SIMD.
+  // W column reads) cannot overtake them.
   union {
     float Wt[n + 1][QS];                         // rows of V^T F, then v^T F
     float Q[d][QS];
   };
-  float Kk[m][W];                                // gains K (box mode: every lane needs all of K)
+  float Kk[KK ? m : 1][W];                       // gains K (box mode: every lane needs all of K)
   // The 4 problems of a half-wave (a b32 read's lane group) read the same
   // relative words; struct strides of 8 mod 16 words put them on 4 disjoint
   // 8-bank sets (16 mod 32 paired them: a 2-way conflict on every column read,
   // 40 % of the sweep's LDS cycles in SQ_LDS_BANK_CONFLICT)
-  static constexpr int kWords = d * QS + m * W;
+  static constexpr int kWords = d * QS + (KK ? m : 1) * W;
   float pad[(8 - kWords % 16 + 16) % 16];
 };
 static_assert(sizeof(Group8Lds<13, 3>) / 4 % 16 == 8, "bank offset between problems");
+static_assert(sizeof(Group8Lds<13, 3, false>) / 4 % 16 == 8, "bank offset between problems");
 
 // Two right-hand sides of group_gains_col at once (columns ja, jb of the gain
 // matrix; j = n is k): the same elimination, each column's own substitution.
@@ -131,8 +140,8 @@ struct Group8Cost {
 // DCONST: every problem of the wave holds a time-invariant diagonal cost in
 // registers (its own instantiation: the caller's rows would keep 32 more
 // registers live across the step)
-template <class Model, int MODE, bool DCONST>
-DEV void group8_sweep(Group8Lds<Model::N, Model::M>& L, int T, int B, int b, int l, bool valid, const Model& md,
+template <class Model, int MODE, bool DCONST, class LdsT>
+DEV void group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Model& md,
                       Group8Cost& cs, const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd,
                       float* __restrict__ ws, float* __restrict__ cpk_out, unsigned char* __restrict__ sym_out) {
   constexpr int n = Model::N, m = Model::M, d = n + m;

@@ -79,13 +79,13 @@ __global__ void __launch_bounds__(64, DILQR_SWEEP_WAVES) k_mpc_sweep_group(int T
 #define DILQR_SWEEP8_WAVES 3
 #endif
 template <class Model, int MODE, bool DCONST>
-__global__ void __launch_bounds__(64, DILQR_SWEEP8_WAVES) k_mpc_sweep_g8(int T, int B, const float* __restrict__ theta,
+__global__ void __launch_bounds__(64, MODE == GAIN_BOX ? 2 : DCONST ? DILQR_SWEEP8_WAVES : 3) k_mpc_sweep_g8(int T, int B, const float* __restrict__ theta,
                                                                          const float* __restrict__ C,
                                                                          const float* __restrict__ c, Bounds bd,
                                                                          int iteration, float eps, int not_improved_lim,
                                                                          int G, MpcState S) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
-  __shared__ Group8Lds<n, m> Ls[kG8PW];
+  __shared__ Group8Lds<n, m, MODE != GAIN_UNC> Ls[kG8PW];
   if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   const bool first = iteration == 0;
   const int l = threadIdx.x & (kG8 - 1), gp = threadIdx.x / kG8;
