@@ -283,8 +283,8 @@ int dilqr_grad_input_f32(int model, int T, int B, const float* X, const float* U
    Later iterations of flagged problems read the copy: 27 instead of 42 floats
    per step at d=6, or 12 for a diagonal cost (diag(q), the reference's own
    callers, il_env.py:159-162); identical arithmetic.  The cost passed to the
-   iterations of one solve must not change.  For the 16-lanes-per-problem
-   models (rocket) Cpk holds B*2d floats instead: iteration 0 sets cost_sym[b]
+   iterations of one solve must not change.  For the lane-group models
+   (rocket) Cpk holds B*2d floats instead: iteration 0 sets cost_sym[b]
    = 7 when problem b's cost is diagonal (off-diagonal entries +0.0) and the
    same at every t, and stores its diag and c [B][2d]; later iterations of
    such problems hold them in registers and read no cost at all.
@@ -367,7 +367,8 @@ int dilqr_mpc_finish_fixed_f32(int T, int m, int B, int iterations, dilqr_mpc_st
    iteration + dilqr_mpc_finish_fixed_f32.  Pendulum and cartpole run begin
    and every iteration in ONE launch (each lane iterates its own problem; no
    problem couples to another until best_du), then the finish launch; rocket
-   keeps its per-iteration launch pairs.  st.du_sq must hold iterations*T*m*B
+   keeps its per-iteration launches (the 8-lane sweep, then the lane-pair
+   line search, each in one instantiation per cost kind).  st.du_sq must hold iterations*T*m*B
    floats and st.best_iter must be set. */
 int dilqr_mpc_solve_fixed_f32(int model, int T, int B, const float* theta, const float* x_init,
                               const float* u_init, const float* C, const float* c,
