@@ -948,6 +948,28 @@ def test_rocket_fused_iteration_equals_unfused_box(golden, bounds):
     assert at_bound > 0.0 and np.abs(u).max() <= bounds[1]
 
 
+def test_rocket_fused_iteration_equals_unfused_tensor_bounds(golden):
+    """Per-(t, b) control bounds ([T, B, m] tensors, the reference's
+    u_lower/u_upper as tensors) through the rocket MPC: the 8-lane sweep's box
+    mode and the lane search read them per step and problem; bit for bit equal
+    to the unfused kernels, with bounds active."""
+    g = golden("mpc_f64")
+    mname, T, it, _b, eps, nil, decay, mls = MPC_CASES["rocket_unc"]
+    x0 = g["rocket_unc_x0"]
+    B, m = x0.shape[0], 3
+    rng = np.random.RandomState(11)
+    half = torch.tensor(rng.uniform(2.0, 8.0, (T, B, m)), dtype=torch.float32)
+    lo, hi = (-half).to(DEV).contiguous(), half.to(DEV).contiguous()
+    a = run_gpu_mpc(x0, mname, T, it, (lo, hi), eps, nil, decay, mls, fused=True)
+    b = run_gpu_mpc(x0, mname, T, it, (lo, hi), eps, nil, decay, mls, fused=False)
+    for ta, tb in zip(a, b):
+        assert same_bits(ta, tb), relerr(cpu(ta), cpu(tb))
+    u = cpu(a[1])
+    at_bound = np.isclose(np.abs(u), half.numpy(), rtol=0, atol=1e-6).mean()
+    print(f"\n[rocket tensor box] controls at their bound: {at_bound:.2f}")
+    assert at_bound > 0.0 and (np.abs(u) <= half.numpy() + 1e-6).all()
+
+
 def test_rocket_mpc_full_size_batch_independence():
     """Config 3 shape (B=32768, T=30): a solve over the whole batch returns, for
     a sample of problems, what solving those problems alone returns."""
