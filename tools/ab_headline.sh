@@ -3,4 +3,4 @@ cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -k "fixed_count or whole_solve or best_du or stop_rule" > gpurun_out/pytest_fin.log 2>&1; rc=$?
 tail -2 gpurun_out/pytest_fin.log; [ $rc -le 1 ] || exit $rc
-AB_CMD="bench.py --no-secondary --no-cpu-baseline --steps 40" timeout -k 10 700 bash tools/ab.sh 4
+AB_CMD="bench.py --no-secondary --no-cpu-baseline --steps 40" timeout -k 10 900 bash tools/ab.sh ${AB_ROUNDS:-4} > gpurun_out/ab_headline.log 2>&1; rc=$?; grep -E "^[a-z0-9_]+ \{" gpurun_out/ab_headline.log | sed -E "s/ \{.*\"value\": ([0-9.]+).*/ \1/"; exit $rc
