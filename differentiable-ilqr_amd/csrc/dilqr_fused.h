@@ -288,8 +288,11 @@ struct FwdIn {
 #define DILQR_PF 1
 #endif
 constexpr int kPF = DILQR_PF;
+// The line search's: 2 was faster with SLP vectorisation on (round 2); in
+// the no-SLP build 1 is (headline A/B, 4 rounds on one box: 1.742e9 ->
+// 1.772e9 problem-iterations/s — one buffer copy per step instead of two).
 #ifndef DILQR_PF_LS
-#define DILQR_PF_LS 2
+#define DILQR_PF_LS 1
 #endif
 constexpr int kPFL = DILQR_PF_LS;                   // the line search's prefetch distance
 
