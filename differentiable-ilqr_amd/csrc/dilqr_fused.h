@@ -580,7 +580,12 @@ DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restric
       if constexpr (kPF >= 2) n1 = n2;
     };
     sweep_step(T - 1, std::true_type{});
-#pragma unroll 2
+// unrolled twice (headline A/B in the no-SLP build, 4 rounds: 1 1.725e9,
+// 2 1.755e9, 3 1.754e9 problem-iterations/s)
+#ifndef DILQR_SWEEP_UNROLL
+#define DILQR_SWEEP_UNROLL 2
+#endif
+#pragma unroll DILQR_SWEEP_UNROLL
     for (int t = T - 2; t >= 0; --t) sweep_step(t, std::false_type{});
     if (sym_out) {
       const unsigned char f = sym ? (unsigned char)(kCostSym | (diag && packed_diag_ok<d>() ? kCostDiag : 0) |
