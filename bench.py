@@ -120,6 +120,28 @@ def cpu_baseline(budget_s=25.0):
                       f"best of 3, {r['elapsed_s']:.1f}s"}
 
 
+def rank_records(tdist, dev, elapsed, lo, hi, props=None):
+    """Each rank's own record, all-gathered after the timed region (never inside
+    it; the data path has no collective): the process group's world size, the
+    device's name, PCI location and UUID, the rank's shard rows and its own
+    elapsed time.  Returned on every rank: {world_size, backend, distinct_devices,
+    elapsed_min_s, elapsed_max_s, spread, per_rank: [...]}."""
+    p = (props or torch.cuda.get_device_properties)(dev)
+    rec = {"rank": tdist.get_rank(), "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": str(dev),
+           "name": p.name, "gcn_arch": p.gcnArchName,
+           "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid),
+           "rows": [int(lo), int(hi)], "elapsed_s": float(elapsed), "host": os.uname().nodename}
+    recs = [None] * tdist.get_world_size()
+    tdist.all_gather_object(recs, rec)
+    recs.sort(key=lambda r: r["rank"])
+    el = [r["elapsed_s"] for r in recs]
+    return {"world_size": tdist.get_world_size(), "backend": tdist.get_backend(),
+            "distinct_devices": len({(r["host"], r["uuid"]) for r in recs}),
+            "rows_cover": all(a["rows"][1] == b["rows"][0] for a, b in zip(recs, recs[1:])),
+            "elapsed_min_s": min(el), "elapsed_max_s": max(el),
+            "spread": (max(el) - min(el)) / max(el) if max(el) > 0 else 0.0, "per_rank": recs}
+
+
 def _timed_solves(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, lqr_iter, solves, warmup_solves):
     """Whole fixed-iteration solves (eps=0, not_improved_lim=inf) -> (problem-iters/s, ms/iteration)."""
     from dilqr import _native as N
@@ -644,10 +666,16 @@ def main():
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
+    ranks = None
     if dist:
+        own = elapsed
         tt = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        # outside the timed region: what each rank ran on, so the line proves
+        # that N ranks solved on N distinct devices (rank_record)
+        ranks = rank_records(tdist, dev, own, lo, hi)
+        assert ranks["world_size"] == world, "WORLD_SIZE disagrees with the process group"
     assert args.kernels_only or bool(torch.isfinite(sv.best_cost).all()), "non-finite costs"
     if args.dump:
         # the last timed solve of this rank's shard (rows [lo, hi) of the global batch)
@@ -757,6 +785,8 @@ def main():
                                  "frac": sweep_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": sweep_bytes,
                                  "avg_launch_ms": sweep_ms},
         }
+        if ranks is not None:
+            line["ranks"] = ranks
         if world == 1 and not args.no_secondary:
             line["secondary"] = secondary_configs(dev)
         if world == 1 and not args.no_cpu_baseline:

@@ -27,6 +27,10 @@ namespace dilqr {
 
 constexpr int kG8 = 8;            // lanes per problem
 constexpr int kG8PW = 64 / kG8;   // problems per wave (= per workgroup)
+// Group8Lds's W/Q union relies on a workgroup being exactly one wave64 (LDS
+// operations of one wave complete in program order): the kernels launch
+// kG8PW * kG8 = 64 threads per workgroup, and gfx950 runs wave64
+static_assert(kG8PW * kG8 == 64, "a group-8 workgroup must be exactly one wave64");
 
 // group_sum's tree over 16 rows with rows l and l+8 in lane l of an 8-lane
 // group: the pairs, quads and half-rows of rows 0-7 (pa) and of rows 8-15 (pb)
@@ -234,6 +238,10 @@ DEV void group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
       qa = cba + Wca[n];
       qb = cbb + Wcb[n];
     }
+    // Q overwrites W^T's words: every lane's W column reads above precede
+    // these stores in the wave's program order (one wave per workgroup), and
+    // the scheduling barrier keeps the compiler from moving them across
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int j = 0; j < d; ++j) { L.Q[ra][j] = QA[j]; L.Q[rb][j] = QB[j]; }
     L.Q[ra][d] = qa;

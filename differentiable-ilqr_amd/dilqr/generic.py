@@ -327,19 +327,20 @@ def slew_augment(mpc, x_init, C, c, F, f, cost, dynamics, x, u):
     return _x_init, _C, _c, _F, _f, _dyn, _cost, _x
 
 
-def solve_subproblem(mpc, x_init, C, c, F, f, cost, dynamics, x, u):
-    """One LQR step of the outer loop (solve_lqr_subproblem, mpc_explicit.py:360-466)."""
+def solve_subproblem(mpc, x_init, C, c, F, f, cost, dynamics, x, u, extras=False):
+    """One LQR step of the outer loop (solve_lqr_subproblem, mpc_explicit.py:360-466).
+    extras: also the step sizes and the pnqp count (the verbose table)."""
     T, n, m = mpc.T, mpc.n_state, mpc.n_ctrl
     if mpc.slew_rate_penalty is None or isinstance(cost, torch.nn.Module):
         return lqr_step_forward(T, n, m, x_init, C, c, F, x, u, cost, dynamics, mpc.u_lower, mpc.u_upper,
                                 mpc.delta_u, mpc.linesearch_decay, mpc.max_linesearch_iter,
-                                getattr(mpc, "u_zero_I", None))
+                                getattr(mpc, "u_zero_I", None), extras=extras)
     _x_init, _C, _c, _F, _f, _dyn, _cost, _x = slew_augment(mpc, x_init, C, c, F, f, cost, dynamics, x, u)
     true_dyn = _dyn if _dyn is not None else LinDx(_F, _f)
-    nx, nu, costs, fdn = lqr_step_forward(T, n + m, m, _x_init, _C, _c, _F, _x, u, _cost, true_dyn, mpc.u_lower,
-                                          mpc.u_upper, mpc.delta_u, mpc.linesearch_decay, mpc.max_linesearch_iter,
-                                          getattr(mpc, "u_zero_I", None))
-    return nx[:, :, m:], nu, costs, fdn
+    out = lqr_step_forward(T, n + m, m, _x_init, _C, _c, _F, _x, u, _cost, true_dyn, mpc.u_lower,
+                           mpc.u_upper, mpc.delta_u, mpc.linesearch_decay, mpc.max_linesearch_iter,
+                           getattr(mpc, "u_zero_I", None), extras=extras)
+    return (out[0][:, :, m:],) + tuple(out[1:])
 
 
 # ---------------------------------------------------------------- the outer loop
@@ -358,7 +359,11 @@ def solve(mpc, x_init, cost, dx, n_batch):
     x_init = x_init.detach()
     best = None
     n_not_improved = 0
-    for _ in range(mpc.lqr_iter):
+    verbose = getattr(mpc, "verbose", 0) > 0
+    if verbose:                                                          # mpc_explicit.py:236-241
+        x0 = rollout(T, u, x_init, dx)
+        print("Initial mean(cost): {:.4e}".format(float(traj_cost(T, x0, u, cost).mean())))
+    for it in range(mpc.lqr_iter):
         u = u.detach()
         x = rollout(T, u, x_init, dx)
         if isinstance(dx, LinDx):
@@ -369,7 +374,8 @@ def solve(mpc, x_init, cost, dx, n_batch):
             C, c = cost.C.detach(), cost.c.detach()
         else:
             C, c, _ = approximate_cost(x, u, cost, diff=False)
-        x, u, costs, full_du_norm = solve_subproblem(mpc, x_init, C, c, F, f, cost, dx, x, u)
+        out = solve_subproblem(mpc, x_init, C, c, F, f, cost, dx, x, u, extras=verbose)
+        x, u, costs, full_du_norm = out[:4]
         n_not_improved += 1
         if best is None:
             best = {"x": x.clone(), "u": u.clone(), "costs": costs.clone(), "fdn": full_du_norm.clone()}
@@ -381,6 +387,11 @@ def solve(mpc, x_init, cost, dx, n_batch):
             best["u"][:, take] = u[:, take]
             best["costs"][take] = costs[take]
             best["fdn"][take] = full_du_norm[take]
+        if verbose:                                                      # mpc_explicit.py:285-295
+            from .util import table_log
+            table_log("lqr", (("iter", it), ("mean(cost)", float(best["costs"].mean()), "{:.4e}"),
+                              ("||full_du||_max", float(full_du_norm.max()), "{:.2e}"),
+                              ("mean(alphas)", float(out[4].mean()), "{:.2e}"), ("total_qp_iters", out[5])))
         if float(full_du_norm.max()) < mpc.eps or n_not_improved > mpc.not_improved_lim:   # 297-299
             break
     return best["x"], best["u"], best["costs"], best["fdn"]

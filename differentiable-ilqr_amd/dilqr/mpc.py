@@ -5,9 +5,11 @@ Module, AUTO_DIFF / FINITE_DIFF linearisation, non-quadratic costs and the
 slew-rate penalty).  The forward loop runs on device; gradients
 flow through a no-op classic LQR step (lqr_step.py:277-282) whose backward is
 the classic adjoint kernel, exactly like mpc.py:302-335.  With model dynamics
-the reference would also differentiate the autograd linearisation
-(mpc.py:538-551); on the HIP path F, f are kernel outputs, so gradients reach
-(x_init, C, c) and, for LinDx, (F, f).
+the reference differentiates the autograd linearisation (mpc.py:538-551): F is
+data, f = dynamics(x, u) - F tau keeps the graph to the model's parameters; here
+F comes from the kernel and, when dx.params requires grad, f is formed the same
+way through the model's device vjp, so gradients reach (x_init, C, c), the
+parameters and, for LinDx, (F, f).
 """
 import warnings
 
@@ -20,6 +22,22 @@ from .definitions import LinDx, QuadCost
 from .lqr_step import LQRStep
 from .mpc_explicit import MPC as ExplicitMPC
 from .mpc_explicit import GradMethods, expand_cost
+
+
+class _RefuseThetaGrad(torch.autograd.Function):
+    """f with a graph to the 5-parameter pendulum's params whose backward
+    raises: the solve runs, a gradient into params is refused rather than
+    silently dropped (the explicit MPC refuses it in its implicit backward)."""
+
+    @staticmethod
+    def forward(ctx, f, params):
+        return f.clone()
+
+    @staticmethod
+    def backward(ctx, gf):
+        raise NotImplementedError("dilqr: gradients into the 5-parameter pendulum's params are not implemented "
+                                  "(no device derivative in theta; the reference's grad_input has no 5-parameter "
+                                  "form either, pendulum.py:157)")
 
 
 class MPC(Module):
@@ -55,6 +73,23 @@ class MPC(Module):
             or (self.grad_method == GradMethods.AUTO_DIFF and getattr(dx, "jacobian_is_autograd", False))))
         return isinstance(cost, QuadCost) and model_ok and self.slew_rate_penalty is None and self.delta_u is None
 
+    def _f_with_params_graph(self, dx, model_id, F, x, u):
+        """f = dynamics(x_t, u_t) - F_t tau_t with the dynamics' graph to its
+        parameters, F a constant — what the reference's AUTO_DIFF linearisation
+        hands the LQR step (mpc.py:538-551: torch.autograd.grad without
+        create_graph gives F as data, new_x keeps the params graph), so a
+        gradient reaches dx.params through f.  The 5-parameter pendulum has no
+        device derivative in theta (its dynamics_vjp is refused), so a
+        gradient there raises instead of being silently dropped."""
+        if model_id == N.MODEL_PENDULUM_COMPLEX:
+            return _RefuseThetaGrad.apply(ops.linearize(model_id, ops.theta_of(dx, x), x, u)[1], dx.params)
+        T, B, n = x.shape
+        m = u.shape[2]
+        xs, us = x[:-1].reshape(-1, n).detach(), u[:-1].reshape(-1, m).detach()
+        new_x = dx(xs, us).view(T - 1, B, n)
+        tau = torch.cat((x[:-1], u[:-1]), 2).detach()
+        return new_x - (F @ tau.unsqueeze(-1)).squeeze(-1)
+
     def forward(self, x_init, cost, dx):
         if not x_init.is_cuda:
             raise RuntimeError("dilqr: x_init must be on the GPU (no CPU path)")
@@ -82,7 +117,7 @@ class MPC(Module):
                     u_init=self.u_init, u_lower=self.u_lower, u_upper=self.u_upper, lqr_iter=self.lqr_iter,
                     eps=self.eps, linesearch_decay=self.linesearch_decay,
                     max_linesearch_iter=self.max_linesearch_iter, not_improved_lim=self.not_improved_lim,
-                    best_cost_eps=self.best_cost_eps)
+                    best_cost_eps=self.best_cost_eps, verbose=self.verbose)
             else:
                 ws = ops.mpc_solve_unfused(model_id, theta, x_init.detach(), C.detach().contiguous(),
                                            c.detach().contiguous(), T, F=Fd, f=fd, u_init=self.u_init,
@@ -90,13 +125,20 @@ class MPC(Module):
                                            eps=self.eps, linesearch_decay=self.linesearch_decay,
                                            max_linesearch_iter=self.max_linesearch_iter,
                                            not_improved_lim=self.not_improved_lim,
-                                           best_cost_eps=self.best_cost_eps, u_zero_I=self.u_zero_I)
-                x, u, costs, full_du_norm = ws.best_x, ws.best_u, ws.best_cost, ws.best_du
+                                           best_cost_eps=self.best_cost_eps, u_zero_I=self.u_zero_I,
+                    verbose=self.verbose)
+                x, u, costs, full_du_norm, _sv = ws.best_x, ws.best_u, ws.best_cost, ws.best_du, ws
+        if self.verbose > 0:                                    # mpc.py:270-275, 368-379
+            from .util import print_solve_log
+            print_solve_log(_sv.log)
         if torch.is_grad_enabled() and self.backprop:
             if lin:
                 F, f = dx.F, (dx.f if dx.f is not None else torch.empty(0, device=x.device))
             else:
                 F, f = ops.linearize(model_id, theta, x, u)
+                params = getattr(dx, "params", None)
+                if isinstance(params, torch.Tensor) and params.requires_grad:
+                    f = self._f_with_params_graph(dx, model_id, F, x, u)
             step = LQRStep(n, m, T, u_lower=self.u_lower, u_upper=self.u_upper, u_zero_I=self.u_zero_I,
                            true_cost=QuadCost(C, c), true_dynamics=dx, current_x=x, current_u=u,
                            back_eps=self.back_eps, no_op_forward=True)

@@ -107,7 +107,8 @@ class MPC(Module):
                     model_id, theta, x_init.detach(), Cd, cd, T, u_init=self.u_init, u_lower=self.u_lower,
                     u_upper=self.u_upper, lqr_iter=self.lqr_iter, eps=self.eps,
                     linesearch_decay=self.linesearch_decay, max_linesearch_iter=self.max_linesearch_iter,
-                    not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps)
+                    not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps,
+                    verbose=self.verbose)
             else:
                 # controls held at zero (mpc_explicit.py:369, 452 -> LQRStep u_zero_I):
                 # the unfused kernels take the mask (masked gain solve, zeroed rollout)
@@ -115,9 +116,13 @@ class MPC(Module):
                     model_id, theta, x_init.detach(), Cd, cd, T, u_init=self.u_init, u_lower=self.u_lower,
                     u_upper=self.u_upper, lqr_iter=self.lqr_iter, eps=self.eps,
                     linesearch_decay=self.linesearch_decay, max_linesearch_iter=self.max_linesearch_iter,
-                    not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps, u_zero_I=self.u_zero_I)
+                    not_improved_lim=self.not_improved_lim, best_cost_eps=self.best_cost_eps, u_zero_I=self.u_zero_I,
+                    verbose=self.verbose)
                 x, u, costs, full_du_norm = sv.best_x, sv.best_u, sv.best_cost, sv.best_du
         self.last_solve = sv
+        if self.verbose > 0:
+            from .util import print_solve_log
+            print_solve_log(sv.log)
 
         need_grad = torch.is_grad_enabled() and self.backprop and (
             C.requires_grad or c.requires_grad or

@@ -352,11 +352,17 @@ class MPCSolve:
 
 def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upper=None, lqr_iter=10,
               eps=1e-7, linesearch_decay=0.2, max_linesearch_iter=10, not_improved_lim=5, best_cost_eps=1e-4,
-              check_every=8):
+              check_every=8, verbose=0):
     """The iLQR outer loop of mpc_explicit.MPC.forward (mpc_explicit.py:228-299)
     entirely on device (fused iterate kernel + norm/stop kernel per iteration);
     the host only polls the stop flag every `check_every` iterations.
-    Returns (best_x, best_u, best_cost, best_du, solve)."""
+    Returns (best_x, best_u, best_cost, best_du, solve).
+
+    verbose > 0: the same launches one iteration per library call, each
+    followed by reductions queued on the stream (mean best cost, max
+    full_du_norm, mean step size: the reference's table row, mpc_explicit.py:
+    285-295) into a device array; `solve.log` holds them for util.print_solve_log
+    (no host sync inside the loop)."""
     B, n = x_init.shape
     m = C.shape[-1] - n
     x_init, C, c = _f32(x_init), _f32(C), _f32(c)
@@ -369,6 +375,12 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
              and plane_bytes <= min(2 ** 31, torch.cuda.mem_get_info(x_init.device)[0] // 16))
     sv = MPCSolve(T, B, n, m, x_init.device, fixed_iters=lqr_iter if fixed else None)
     bounds, keep = N.make_bounds(u_lower, u_upper)
+    if verbose > 0:
+        _mpc_solve_logged(sv, model_id, theta, x_init, C, c, u_init, bounds, u_lower is None, lqr_iter, eps,
+                          linesearch_decay, max_linesearch_iter, not_improved_lim, best_cost_eps)
+        del keep
+        x, u = sv.gather_best()
+        return x, u, sv.best_cost, sv.best_du, sv
     if fixed:
         sv.solve_fixed(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, best_cost_eps,
                        u_init)
@@ -387,6 +399,48 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     del keep
     x, u = sv.gather_best()
     return x, u, sv.best_cost, sv.best_du, sv
+
+
+def quad_traj_cost(x, u, C, c):
+    """util.get_cost for a quadratic cost (util.py:130-153): per problem,
+    sum_t 0.5 tau_t^T C_t tau_t + c_t^T tau_t, in torch on the device (the
+    verbose report's initial cost only)."""
+    tau = torch.cat((x, u), -1)
+    return (0.5 * torch.einsum("tbi,tbij,tbj->tb", tau, C, tau) + (tau * c).sum(-1)).sum(0)
+
+
+def _mpc_solve_logged(sv, model_id, theta, x_init, C, c, u_init, bounds, unbounded, lqr_iter, eps, decay, max_ls,
+                      not_improved_lim, best_cost_eps):
+    """mpc_solve with verbose > 0: the same kernels, one iteration per call,
+    the table row's reductions queued after each on the launch stream."""
+    dev = x_init.device
+    stats = torch.zeros(max(lqr_iter, 1), 3, device=dev)
+    sv.begin(model_id, theta, x_init, u_init)
+    x0, u0 = sv.gather_best()                               # slot 0: get_traj(u_init)
+    initial = quad_traj_cost(x0, u0, C, c).mean()
+    T, m, B = sv.T, sv.m, sv.B
+    for i in range(lqr_iter):
+        if sv.fixed_iters:
+            sv.iterate_fixed(model_id, theta, x_init, C, c, bounds, decay, max_ls, i, best_cost_eps)
+            fdn = quirk_norm(sv.du_sq[i * T:(i + 1) * T])
+        else:
+            sv.iterate(model_id, theta, x_init, C, c, bounds, decay, max_ls, i, best_cost_eps, eps, not_improved_lim)
+            fdn = sv.full_du_norm
+        stats[i, 0] = sv.best_cost.mean()
+        stats[i, 1] = fdn.max()
+        stats[i, 2] = sv.alpha.mean()
+    if sv.fixed_iters:
+        sv.finish_fixed(lqr_iter)
+    # the iterations that ran: the rule after iteration k is applied by
+    # iteration k+1's prologue, which then publishes iter = k+1 with the stop
+    # flag (dilqr_fused.h mpc_decide); a solve that never stopped ran them all
+    ran = lqr_iter
+    if not sv.fixed_iters and lqr_iter > 1 and sv.stopped:
+        ran = sv.iterations
+    # total_qp_iters: 0 without bounds, as the reference (pnqp runs only with
+    # bounds, lqr_step_explicit.py:137-150); the fused kernels do not count the
+    # batch-coupled pnqp iterations the reference reports with bounds
+    sv.log = {"initial_mean_cost": initial, "stats": stats, "iterations": ran, "qp_iters": 0 if unbounded else None}
 
 
 def lqr_adjoint(C, c, F, x, u, dl_dx, dl_du, u_lower=None, u_upper=None, m_solver=N.SOLVE_INV, want_df=True):
@@ -412,7 +466,7 @@ def lqr_adjoint(C, c, F, x, u, dl_dx, dl_du, u_lower=None, u_upper=None, m_solve
 
 def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=None, u_lower=None,
                       u_upper=None, lqr_iter=10, eps=1e-7, linesearch_decay=0.2, max_linesearch_iter=10,
-                      not_improved_lim=5, best_cost_eps=1e-4, check_every=8, u_zero_I=None):
+                      not_improved_lim=5, best_cost_eps=1e-4, check_every=8, u_zero_I=None, verbose=0):
     """The same outer loop with the unfused kernels (linearise -> F in HBM ->
     Riccati -> rollout/line search).  Used for LinDx dynamics (classic mpc.MPC,
     the adjoint engines), MPC(u_zero_I=...) and to cross-check the fused
@@ -442,6 +496,11 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
     zI = zero_mask(u_zero_I, T, B, m, dev)
     N.call("dilqr_rollout_f32", model_id, n, m, T, B, N.ptr(theta), N.ptr(F), N.ptr(f), N.ptr(x_init),
            N.ptr(ws.ua), N.ptr(ws.xa), s)
+    stats = None
+    if verbose > 0:                        # the table rows, reduced on the stream (util.print_solve_log)
+        stats = torch.zeros(max(lqr_iter, 1), 3, device=dev)
+        initial = quad_traj_cost(ws.xa, ws.ua, C, c).mean()
+    ran = 0
     for i in range(lqr_iter):
         if model_id == N.MODEL_LINDX:
             Fi, fi = F, f
@@ -462,6 +521,11 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
                N.ptr(ws.du_sq), N.ptr(ws.fdn), N.ptr(ws.best_x), N.ptr(ws.best_u), N.ptr(ws.best_cost),
                N.ptr(ws.best_du), N.ptr(ws.ctrl), s)
         del keep
+        if stats is not None:
+            stats[i, 0] = ws.best_cost.mean()
+            stats[i, 1] = ws.fdn.max()
+            stats[i, 2] = ws.alpha.mean()
+        ran = i + 1
         ws.xa, ws.xb = ws.xb, ws.xa
         ws.ua, ws.ub = ws.ub, ws.ua
         # once the stop rule fired, k_mpc_best ignores further iterations (the
@@ -470,4 +534,11 @@ def mpc_solve_unfused(model_id, theta, x_init, C, c, T, F=None, f=None, u_init=N
         # only every check_every iterations, like mpc_solve
         if check_every and (i + 1) % check_every == 0 and i + 1 < lqr_iter and int(ws.ctrl[1].item()):
             break
+    if stats is not None:
+        # k_mpc_control counts the iterations that ran (ctrl[0]) and stops counting
+        # once the rule fired (ctrl[1])
+        if int(ws.ctrl[1].item()):
+            ran = min(ran, int(ws.ctrl[0].item()))
+        ws.log = {"initial_mean_cost": initial, "stats": stats, "iterations": ran,
+                  "qp_iters": 0 if u_lower is None else None}
     return ws

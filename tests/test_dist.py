@@ -138,6 +138,42 @@ def test_sharded_stop_rule_is_per_shard(tmp_path):
     assert not np.array_equal(np.concatenate([s["du"] for s in per_shard]), du_w)
 
 
+def _rank_record_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["LOCAL_RANK"] = str(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import json
+    import types
+    import bench
+    fake = lambda dev: types.SimpleNamespace(  # noqa: E731  (a device per rank, as the driver's N-GPU node)
+        name="AMD Instinct MI355X", gcnArchName="gfx950:sramecc+:xnack-", pci_domain_id=0, pci_bus_id=0x10 + rank,
+        pci_device_id=0, uuid=f"GPU-{rank:04d}")
+    lo, hi = bench.shard_rows(64 * world, world, rank)
+    rec = bench.rank_records(dist, f"cuda:{rank}", 0.5 + rank, lo, hi, props=fake)
+    if rank == 0:
+        with open(os.path.join(out_dir, "ranks.json"), "w") as f:
+            json.dump(rec, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_records_gloo_world2(tmp_path):
+    """bench.py's self-verifying N > 1 record (outside the timed region): the
+    process group's world size, one entry per rank with its device, PCI
+    location, shard rows and own elapsed time, and the min/max spread."""
+    import json
+    world = 2
+    mp.spawn(_rank_record_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    rec = json.load(open(tmp_path / "ranks.json"))
+    assert rec["world_size"] == world and rec["backend"] == "gloo" and rec["distinct_devices"] == world
+    assert [r["rank"] for r in rec["per_rank"]] == [0, 1]
+    assert [r["pci"] for r in rec["per_rank"]] == ["0000:10:00", "0000:11:00"]
+    assert rec["rows_cover"] and rec["per_rank"][1]["rows"] == [64, 128]
+    assert rec["elapsed_min_s"] == 0.5 and rec["elapsed_max_s"] == 1.5
+    assert rec["spread"] == pytest.approx(1.0 / 1.5)
+
+
 def test_shard_rows_cover_batch():
     import bench
     for world in (1, 2, 4, 8):
@@ -166,6 +202,14 @@ def test_bench_sharded_hip_path_equals_whole_batch(tmp_path):
            "--no-secondary", "--no-cpu-baseline", "--dump", str(tmp_path)]
     r = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    rk = line["ranks"]                      # the self-verifying record (both ranks share cuda:0 here)
+    assert line["n_gpus"] == world and rk["world_size"] == world and rk["backend"] == "gloo"
+    assert [p["rank"] for p in rk["per_rank"]] == list(range(world)) and rk["distinct_devices"] == 1
+    assert rk["rows_cover"] and rk["per_rank"][-1]["rows"][1] == B_per * world
+    assert rk["elapsed_max_s"] == pytest.approx(line["ms_per_step"] * line["steps"] / 1e3, rel=1e-9)
+    assert all(p["gcn_arch"].startswith("gfx950") and p["pci"] for p in rk["per_rank"])
     import bench
     from dilqr import ops
     from dilqr import _native as N
@@ -207,3 +251,7 @@ def test_bench_rccl_path_runs(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 1 and line["value"] > 0 and line["config"]["global_batch"] == 4096
+    rk = line["ranks"]
+    assert rk["world_size"] == 1 and rk["backend"] == "nccl" and rk["distinct_devices"] == 1
+    assert rk["per_rank"][0]["rows"] == [0, 4096] and rk["per_rank"][0]["gcn_arch"].startswith("gfx950")
+    assert rk["elapsed_min_s"] == rk["elapsed_max_s"] > 0

@@ -1,0 +1,187 @@
+"""API-fidelity tests of the MPC classes on the GPU (round 5):
+
+  * `verbose > 0` prints the reference's per-iteration table
+    (mpc_explicit.py:236-241, 285-295; util.table_log, util.py:80-101) from
+    figures the device recorded, one row per iteration the solve ran;
+  * the classic mpc.MPC sends a gradient into an env_dx model's params the
+    way the reference's AUTO_DIFF linearisation does (mpc.py:538-551: F as
+    data, f = dynamics(x, u) - F tau with the params graph), and refuses it for
+    the 5-parameter pendulum instead of dropping it.
+"""
+import re
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def cartpole_case(B, T, seed=0):
+    from dilqr.env_dx.cartpole import CartpoleDx
+    rng = np.random.RandomState(seed)
+    th = rng.uniform(-np.pi, np.pi, B)
+    x0 = np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                   rng.uniform(-1, 1, B)], 1)
+    dx = CartpoleDx()
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV)
+    c = p.repeat(T, B, 1).to(DEV)
+    return dx, torch.tensor(x0, dtype=torch.float32, device=DEV), C, c
+
+
+ROW = re.compile(r"^\| (\d+) \| (\S+) \| (\S+) \| (\S+) \| (\S+) \|$")
+
+
+@pytest.mark.parametrize("mode", ["stop_rule", "fixed", "box", "u_zero_I"])
+def test_verbose_table(capsys, mode):
+    """The verbose report: 'Initial mean(cost)', the table header once, then one
+    row per iteration that ran; the last row's mean(cost) is the returned costs'
+    mean and every row's figures are finite.  A verbose solve returns the same
+    bits as a quiet one (the same launches, one iteration per call)."""
+    import dilqr
+    from dilqr import util
+    util._seen_tables.discard("lqr")
+    T, B = 12, 256
+    dx, x0, C, c = cartpole_case(B, T)
+    kw = dict(lqr_iter=8, exit_unconverged=False, detach_unconverged=False, linesearch_decay=0.5,
+              max_linesearch_iter=2)
+    if mode == "stop_rule":
+        kw.update(eps=1e-2, not_improved_lim=3)
+    elif mode == "fixed":
+        kw.update(eps=0.0, not_improved_lim=10 ** 9)
+    elif mode == "box":
+        kw.update(eps=1e-3, u_lower=-2.0, u_upper=2.0)
+    else:
+        zI = torch.zeros(T, B, 1, dtype=torch.bool, device=DEV)
+        zI[-3:] = True
+        kw.update(eps=1e-3, u_zero_I=zI)
+    quiet = dilqr.MPC(5, 1, T, verbose=0, **kw)
+    loud = dilqr.MPC(5, 1, T, verbose=1, **kw)
+    with torch.no_grad():
+        xq, uq, cq = quiet(x0, dilqr.QuadCost(C, c), dx)
+        capsys.readouterr()
+        xv, uv, cv = loud(x0, dilqr.QuadCost(C, c), dx)
+    out = capsys.readouterr().out.strip().splitlines()
+    assert torch.equal(xq, xv) and torch.equal(uq, uv) and torch.equal(cq, cv)
+    assert out[0].startswith("Initial mean(cost): ")
+    assert np.isfinite(float(out[0].split(":")[1]))
+    assert out[1] == "| iter | mean(cost) | ||full_du||_max | mean(alphas) | total_qp_iters |"
+    rows = [ROW.match(l) for l in out[2:]]
+    assert rows and all(rows), out
+    its = [int(r.group(1)) for r in rows]
+    assert its == list(range(len(its)))
+    sv = loud.last_solve
+    assert len(its) == sv.log["iterations"]
+    if mode == "fixed":
+        assert len(its) == 8
+    last = rows[-1]
+    assert float(last.group(2)) == pytest.approx(float(cv.mean()), rel=1e-4)
+    for r in rows:
+        assert np.isfinite(float(r.group(3))) and np.isfinite(float(r.group(4)))
+        assert r.group(5) == ("-" if mode == "box" else "0")
+    print(f"verbose {mode}: {len(its)} rows")
+
+
+def test_verbose_log_fused_equals_unfused():
+    """The fused loop (stop rule on device, decision applied by the next
+    iteration's prologue) and the unfused host-stepped loop (k_mpc_control
+    after every iteration) record the same rows: the same iteration count and
+    the same per-iteration figures (their iterates agree bit for bit,
+    test_fused_iteration_equals_unfused)."""
+    from dilqr import _native as N
+    from dilqr import ops
+    T, B = 10, 128
+    dx, x0, C, c = cartpole_case(B, T, seed=3)
+    th = ops.theta_of(dx, x0)
+    for eps, lim in ((5e-2, 5), (1e-6, 1)):
+        kw = dict(lqr_iter=12, eps=eps, linesearch_decay=0.5, max_linesearch_iter=2, not_improved_lim=lim,
+                  verbose=1)
+        sv = ops.mpc_solve(N.MODEL_CARTPOLE, th, x0, C.contiguous(), c.contiguous(), T, **kw)[4]
+        ws = ops.mpc_solve_unfused(N.MODEL_CARTPOLE, th, x0, C.contiguous(), c.contiguous(), T, **kw)
+        a, b = sv.log, ws.log
+        print(f"eps {eps} lim {lim}: fused {a['iterations']} rows, unfused {b['iterations']}")
+        assert a["iterations"] == b["iterations"]
+        k = a["iterations"]
+        assert torch.allclose(a["stats"][:k], b["stats"][:k], rtol=1e-6, atol=0)
+        assert float(a["initial_mean_cost"]) == pytest.approx(float(b["initial_mean_cost"]), rel=1e-6)
+
+
+def test_classic_mpc_params_gradient_matches_autodiff():
+    """Classic mpc.MPC, cartpole with params requiring grad: the fused
+    (ANALYTIC) path's gradient into params equals the generic AUTO_DIFF path's
+    (the reference's wiring, mpc.py:538-551) at the same solution.  Before
+    round 5 the fused path left params.grad None."""
+    from dilqr import mpc as cmpc
+    from dilqr.env_dx.cartpole import CartpoleDx
+    T, B = 10, 16
+    _, x0, C, c = cartpole_case(B, T, seed=1)
+    grads = {}
+    sols = {}
+    for gm in (cmpc.GradMethods.ANALYTIC, cmpc.GradMethods.AUTO_DIFF):
+        params = torch.tensor((9.8, 1.0, 0.1, 0.5), device=DEV, requires_grad=True)
+        dx = CartpoleDx(params)
+        m = cmpc.MPC(5, 1, T, lqr_iter=20, eps=1e-5, grad_method=gm, exit_unconverged=False,
+                     detach_unconverged=False, linesearch_decay=0.5, max_linesearch_iter=2, n_batch=B)
+        x, u, _ = m(x0, cmpc.QuadCost(C, c), dx)
+        w = torch.linspace(-1, 1, T * B, device=DEV).view(T, B, 1)
+        (u * w).sum().backward()
+        assert params.grad is not None, gm
+        grads[gm] = params.grad.detach().cpu().numpy().astype(np.float64)
+        sols[gm] = u.detach().cpu().numpy()
+    a, b = grads[cmpc.GradMethods.ANALYTIC], grads[cmpc.GradMethods.AUTO_DIFF]
+    du = np.max(np.abs(sols[cmpc.GradMethods.ANALYTIC] - sols[cmpc.GradMethods.AUTO_DIFF]))
+    err = np.max(np.abs(a - b)) / max(1.0, np.max(np.abs(b)))
+    print(f"classic params grad: fused {a}, generic {b}, rel err {err:.2e} (solutions differ by {du:.2e})")
+    assert np.all(np.isfinite(a)) and np.any(a != 0)
+    assert err < 1e-3
+
+
+def test_classic_mpc_pendulum_complex_params_gradient_refused():
+    """The 5-parameter pendulum through the classic MPC: the solve runs, a
+    backward into params raises (no device derivative in theta) instead of
+    leaving params.grad silently None."""
+    from dilqr import mpc as cmpc
+    from dilqr.env_dx.pendulum import PendulumDx
+    from oracle import models as omodels
+    dx = PendulumDx(torch.tensor(omodels.PendulumComplex.default_params), simple=False)
+    dx.params = dx.params.clone().to(DEV).requires_grad_(True)
+    T, B = 5, 4
+    q, p = dx.get_true_obj()
+    m = cmpc.MPC(3, 1, T, u_lower=-2.0, u_upper=2.0, lqr_iter=3, exit_unconverged=False, detach_unconverged=False)
+    x0 = torch.tensor(np.tile([1.0, 0.0, 0.0], (B, 1)), dtype=torch.float32, device=DEV)
+    x, u, _ = m(x0, cmpc.QuadCost(torch.diag(q).repeat(T, B, 1, 1).to(DEV), p.repeat(T, B, 1).to(DEV)), dx)
+    with pytest.raises(NotImplementedError, match="5-parameter"):
+        u.sum().backward()
+
+
+@pytest.mark.parametrize("name,n,m", [("pendulum", 3, 1), ("cartpole", 5, 1), ("rocket", 13, 3)])
+def test_qp_total_vs_golden_and_per_step_maxima(golden, name, n, m):
+    """LQRStep's n_total_qp_iter (ops.lqr_backward qp_total: the per-step batch
+    maximum of the pnqp iterations from the sweep's atomic max, plus 1 per step,
+    lqr_step_explicit.py:137-150) on the reference's bounded Riccati case
+    (riccati golden, box +-1): equal to the per-problem oracle's
+    sum_t (1 + max_b it[t, b]) exactly, and to the reference's own batch-coupled
+    count (its Armijo loop exits on the batch max, pnqp.py:75; parity of the
+    count is then by this case: the golden's value).  rocket (m = 3) takes the
+    16-lane group sweep, the others the one-lane sweep."""
+    from dilqr import ops
+    from oracle import lqr as olqr
+    g = golden("riccati_f64")
+    C, c, F, u = g[f"{name}_C"], g[f"{name}_c"], g[f"{name}_F"], g[f"{name}_u"]
+    dev = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=DEV)  # noqa: E731
+    _, _, total = ops.lqr_backward(dev(C), dev(c), dev(F), n, m, u=dev(u), u_lower=-1.0, u_upper=1.0,
+                                   qp_total=True)
+    _, _, o_total = olqr.lqr_backward(C, c, F, n, m, u=u, u_lower=-1.0, u_upper=1.0, per_problem=True)
+    ref = int(g[f"{name}_box_nqp"])
+    print(f"{name}: qp_total {total}, per-problem oracle {o_total}, reference {ref}")
+    assert total == o_total
+    assert total == ref

@@ -996,8 +996,13 @@ def test_rocket_mpc_full_size_batch_independence():
     assert torch.isfinite(cost).all()
     idx = np.array([0, 1, 4097, 12345, B - 1])
     xs, us, cs = solve(x0[idx])
-    assert relerr(cpu(cost[idx]), cpu(cs)) < 1e-5
-    assert relerr(cpu(u[:, idx]), cpu(us)) < 1e-4
+    print(f"rocket batch independence: max |du| {float((u[:, idx] - us).abs().max()):.3e}, "
+          f"max |dcost| {float((cost[idx] - cs).abs().max()):.3e}")
+    # bit for bit, as cartpole's (fixed-count solves are batch-independent,
+    # SURVEY.md §4 item 4): no path of the 8-lane sweep, the lane-pair search or
+    # the gain-record layout may depend on B
+    idx_t = torch.tensor(idx, device=DEV)
+    assert torch.equal(cost[idx_t], cs) and torch.equal(u[:, idx_t], us) and torch.equal(x[:, idx_t], xs)
 
 
 # ------------------------------------------------------------------ standalone fused iteration
