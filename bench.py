@@ -258,6 +258,32 @@ FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: peak FP32 (vector)
 PMC_COMMIT = [None]
 
 
+# VALU issue ceilings (tools/microbench/valu_issue.hip, profiles/r02/valu_issue.log,
+# re-measured in profiles/r05/valu_issue.log): independent v_fma_f32 wave-instructions
+# per second per SIMD with 1, 2 and 4 waves resident per SIMD
+VALU_ISSUE_PER_SIMD = {1: 320000 / 0.817e-3, 2: 640000 / 1.300e-3, 4: 1280000 / 2.384e-3}
+N_SIMD = 1024                 # 256 CUs x 4 SIMDs
+
+
+def issue_roofline(pmc_entry, n_waves, ms):
+    """The issue roofline of a launch: VALU wave-instructions per SIMD per second
+    (PMC SQ_INSTS_VALU per wave x waves per SIMD / the launch time) against the
+    microbenchmark's independent-FMA issue rate at the same residency (1 wave
+    per SIMD for the one-lane-per-problem solve) and the saturated rate."""
+    vi = pmc_entry.get("valu_instr_per_wave")
+    if not vi:
+        return None
+    wps = n_waves / N_SIMD
+    achieved = vi * wps / (ms * 1e-3)
+    res = min(VALU_ISSUE_PER_SIMD, key=lambda k: abs(k - max(wps, 1.0)))
+    peak = VALU_ISSUE_PER_SIMD[res]
+    return {"unit": "VALU wave-instr/s per SIMD", "valu_instr_per_wave": vi, "waves_per_simd": wps,
+            "achieved": achieved, "peak": peak, "peak_residency_waves": res, "frac": achieved / peak,
+            "peak_saturated": VALU_ISSUE_PER_SIMD[4], "frac_of_saturated": achieved / VALU_ISSUE_PER_SIMD[4],
+            "source": "PMC valu_instr_per_wave (profiles/pmc_traffic.json) x waves / avg launch time; peaks from "
+                      "tools/microbench/valu_issue.hip"}
+
+
 def load_pmc():
     """profiles/pmc_traffic.json -> {kernel signature: counters} (tools/pmc_summary.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -770,7 +796,8 @@ def main():
                          "algorithmic_bytes_per_launch": solve_bytes, "avg_launch_ms": solve_ms,
                          "limiter": {"what": "VALU issue at one wave per SIMD (B=65536 = 1024 waves); not HBM",
                                      **{k: v for k, v in head_pmc.items()
-                                        if k not in ("hbm_bytes_per_launch", "measured_at")}}},
+                                        if k not in ("hbm_bytes_per_launch", "measured_at")}},
+                         "issue": issue_roofline(head_pmc, (B + 63) // 64, solve_ms)},
             "roofline_steady_iteration": {
                 "kernel": "k_mpc_iterate<Cartpole,UNC,LDS gains,steady> (the stop-rule path's per-iteration launch; "
                           + cost_path + ")",
