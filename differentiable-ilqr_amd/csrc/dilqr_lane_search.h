@@ -91,7 +91,7 @@ DEV float lane_stage_cost(const float (&tau)[d], const float (&cd)[d], const flo
 #ifndef DILQR_SEARCH_PFD
 #define DILQR_SEARCH_PFD 1
 #endif
-template <class Model, int BM, bool DCONST>
+template <class Model, int BM, bool DCONST, int PFD = DILQR_SEARCH_PFD>
 DEV void lane_pass(int T, int B, int b, const Model& md, const float* __restrict__ x_init,
                    const float (&cd)[Model::N + Model::M], const float (&cc)[Model::N + Model::M],
                    const float* __restrict__ C, const float* __restrict__ c, const float* __restrict__ ws,
@@ -151,7 +151,7 @@ DEV void lane_pass(int T, int B, int b, const Model& md, const float* __restrict
   // PFD 1 0.339-0.351 ms per MPC iteration, 2 0.356-0.368, 3 0.358-0.364 —
   // a search round streams ~360 MB (gain records, the current trajectory, two
   // candidates out) at ~5 TB/s, so deeper prefetch only adds registers.
-  constexpr int P = DILQR_SEARCH_PFD + 1;
+  constexpr int P = PFD + 1;
   LaneIn<n, m, GREC> ring[P];
 #pragma unroll
   for (int i = 0; i < P - 1; ++i)
@@ -242,6 +242,106 @@ __global__ void __launch_bounds__(64) k_mpc_search_lane(int T, int B, const floa
   S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
   if (S.best_iter && (first || better)) S.best_iter[b] = iteration;       // fixed-count solves
   S.slot[b] = (unsigned char)nw;
+}
+
+// The same line search on a QUAD of lanes per problem (16 problems per wave):
+// lane j of the quad rolls pass p = 4r + j of round r out for its COST only, so
+// one round decides up to four passes and the gain records and the current
+// trajectory are read once per round for all of them (the quad's lanes read
+// the same addresses).  Pass 0 (lane 0) also writes its trajectory to slot sa,
+// speculatively: it is the winner in most early iterations.  The last pass
+// (p = max_ls - 1) is accepted whatever its cost (lqr_step_explicit.py:252), so
+// it is never rolled out to be compared.  When the winner is not pass 0, lane 0
+// of the quad rolls the winner's step size out again with writes (phase 2; the
+// same function on the same inputs: the same bits).  So the search returns the
+// sequential search's pass, cost, step size and trajectory bit for bit, like
+// k_mpc_search_lane, with one round (and at most one rewrite) where the pairs
+// took up to three rounds (max_ls = 5), two waves per SIMD at config 3 where
+// the pairs had one, and no second candidate stream to HBM.
+#ifndef DILQR_QUAD_PFD
+#define DILQR_QUAD_PFD 0
+#endif
+#ifndef DILQR_QUAD_WAVES
+#define DILQR_QUAD_WAVES 2
+#endif
+template <class Model, int BM, bool DCONST>
+__global__ void __launch_bounds__(64, DCONST ? DILQR_QUAD_WAVES : 1) k_mpc_search_quad(int T, int B, const float* __restrict__ theta,
+                                                        const float* __restrict__ x_init,
+                                                        const float* __restrict__ C, const float* __restrict__ c,
+                                                        Bounds bd, float decay, int max_ls, int iteration,
+                                                        float best_cost_eps, int G, MpcState S) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  if (iteration > 0 && G >= 0 && S.ctrl[iteration & 1].stopped) return;
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = tid >> 2, j = tid & 3;
+  if (b >= B) return;                                          // a whole quad
+  Model md; md.load(theta);
+  const bool first = iteration == 0;
+  const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
+  const int cur = S.slot[b], best = S.slot[B + b];
+  int sa, sb;
+  free_slots(cur, best, sa, sb);
+  const float* x = S.Xs + cur * TBn;
+  const float* u = S.Us + cur * TBm;
+  float* xo = S.Xs + sa * TBn;
+  float* uo = S.Us + sa * TBm;
+  const bool dconst = S.Cpk && S.cost_sym[b] == 7;
+  float cd[d], cc[d];
+#pragma unroll
+  for (int r = 0; r < d; ++r) { cd[r] = 0.f; cc[r] = 0.f; }
+  if (dconst) {
+    ld(cd, S.Cpk + (size_t)b * 2 * d);
+    ld(cc, S.Cpk + (size_t)b * 2 * d + d);
+  }
+  if (__all(dconst) != DCONST) return;                         // wave-uniform, as k_mpc_search_lane
+  const int q0 = (threadIdx.x & 63) & ~3;                      // the quad's first lane
+  const int last = max_ls - 1;
+  // alpha_p = decay^p by the sequential search's chain of products (249)
+  float al = 1.f;
+  for (int i = 0; i < j; ++i) al *= decay;
+  float old_cost = 0.f, cost = 0.f;
+  int win = -1;                                                // the accepted pass (quad-uniform)
+  for (int p0 = 0;; p0 += 4) {
+    const int p = p0 + j;
+    // lane 0 of round 0 always rolls pass 0 out (with writes, and the du rows
+    // of the reference's full_du_norm); other passes only to be compared
+    const bool roll = (p == 0) || (p < last);
+    float cm = 0.f, oc = 0.f;
+    if (roll)
+      lane_pass<Model, BM, DCONST, DILQR_QUAD_PFD>(T, B, b, md, x_init, cd, cc, C, c, S.ws, x, u, bd, al, p == 0,
+                                                   xo, uo, p == 0 ? S.du_sq : nullptr, cm, oc);
+    if (p0 == 0) old_cost = __shfl(oc, q0, 64);                // every pass sums the same old cost; lane 0's
+    // the first pass of this round that is accepted: cost <= old, or the last
+    const bool acc = p <= last && ((roll && !(cm > old_cost)) || p == last);
+    const unsigned long long bal = __ballot(acc);
+    const unsigned qb = (unsigned)(bal >> q0) & 15u;
+    if (qb) {
+      const int k = __builtin_ctz(qb);
+      win = p0 + k;
+      cost = __shfl(cm, q0 + k, 64);                           // a rolled pass's cost (the last: phase 2)
+      break;
+    }
+    for (int i = 0; i < 4; ++i) al *= decay;                   // this lane's pass of the next round
+  }
+  // alpha of the accepted pass, the same chain
+  float aw = 1.f;
+  for (int i = 0; i < win; ++i) aw *= decay;
+  if (j != 0) return;
+  if (win != 0) {                                              // phase 2: the winner's trajectory
+    float oc;
+    lane_pass<Model, BM, DCONST, DILQR_QUAD_PFD>(T, B, b, md, x_init, cd, cc, C, c, S.ws, x, u, bd, aw, true, xo,
+                                                 uo, nullptr, cost, oc);
+  }
+  S.cost[b] = cost;
+  S.alpha[b] = aw;
+  const bool better = !first && (cost <= S.best_cost[b] + best_cost_eps);   // mpc_explicit.py:278
+  if (first || better) {
+    S.best_cost[b] = cost;
+    S.slot[B + b] = (unsigned char)sa;
+  }
+  S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
+  if (S.best_iter && (first || better)) S.best_iter[b] = iteration;       // fixed-count solves
+  S.slot[b] = (unsigned char)sa;
 }
 
 }  // namespace dilqr

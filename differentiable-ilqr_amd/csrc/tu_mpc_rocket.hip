@@ -117,10 +117,21 @@ __global__ void __launch_bounds__(64, MODE == GAIN_BOX ? 2 : DCONST ? DILQR_SWEE
 #ifndef DILQR_SWEEP_LANES
 #define DILQR_SWEEP_LANES 8
 #endif
+// DILQR_SEARCH_QUAD: the line search on a quad of lanes per problem (1, the
+// default: every pass of a round at once, cost only) or on lane pairs (0)
+#ifndef DILQR_SEARCH_QUAD
+#define DILQR_SEARCH_QUAD 1
+#endif
 int launch_mpc_step_rocket(const MpcStepArgs& a) {
+#if DILQR_SEARCH_QUAD
+#define SEARCH(BM_, DC_)                                                                                          \
+  k_mpc_search_quad<Rocket, BM_, DC_><<<grid_for(4 * (long long)a.B), kBlock, 0, a.stream>>>(                     \
+      a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st)
+#else
 #define SEARCH(BM_, DC_)                                                                                          \
   k_mpc_search_lane<Rocket, BM_, DC_><<<grid_for(2 * (long long)a.B), kBlock, 0, a.stream>>>(                     \
       a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st)
+#endif
 #if DILQR_SWEEP_LANES == 8
 #define SWEEP8(MODE_, DC_)                                                                                        \
   k_mpc_sweep_g8<Rocket, MODE_, DC_><<<(int)((a.B + kG8PW - 1) / kG8PW), 64, 0, a.stream>>>(                     \

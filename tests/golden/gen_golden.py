@@ -530,6 +530,21 @@ def case_il():
             setattr(env, k, torch.tensor(tensors[k], dtype=torch.float32))
         il_exp.pkl = types.SimpleNamespace(load=lambda f, _e=env: _e, dump=lambda *a, **k: None)
         work = tempfile.mkdtemp()
+        lin = R.mpc_explicit.MPC.linearize_dynamics
+        if mode == "empc":
+            # SURVEY.md §8(c) implicit-backward recipe inside the reference's own
+            # MPC: the closing linearisation (mpc_explicit.py:302-310) gets the
+            # best iterate detached.  The reference makes x, u fresh leaves
+            # (.detach().requires_grad_(True)) whose views get_linear_dyn then
+            # writes through, which torch 2.10 refuses at backward ("leaf
+            # variable has been moved into the graph interior"); those leaves'
+            # gradients are consumed by nothing, so detaching them changes no
+            # gradient that reaches the parameters (F is built from
+            # params.detach(), f = dynamics(x, u) - F tau keeps the params graph,
+            # and the no-op LQRStep gets theta = dx.params, 325).
+            def lin_detached(self, x, u, dynamics, diff, _lin=lin):
+                return _lin(self, x.detach() if diff else x, u.detach() if diff else u, dynamics, diff)
+            R.mpc_explicit.MPC.linearize_dynamics = lin_detached
         try:
             exp = il_exp.IL_Exp(data=os.path.join(REF, "data", ds + ".pkl"), work=work, save=os.path.join(work, "s"),
                                 n_batch=n_batch, mode=mode, learn_cost=lc, learn_dx=ldx, no_cuda=True, seed=5,
@@ -548,6 +563,7 @@ def case_il():
             print(f"  {name}: reference raised {type(e).__name__}: {e}")
             out[f"{name}_error"] = np.array(f"{type(e).__name__}: {e}")
         finally:
+            R.mpc_explicit.MPC.linearize_dynamics = lin
             shutil.rmtree(work, ignore_errors=True)
     save("il", **out)
 
