@@ -41,5 +41,8 @@ for i in range(10):
     # a 4-lanes-per-problem search: 16 problems per wave, one round of 4 candidates
     w16 = al.view(-1, 16)
     q2 = float((w16 < 0.008 - 1e-9).any(1).float().mean())
+    # the quad search (k_mpc_search_quad): a wave rewrites (phase 2) when any
+    # of its 16 problems accepted a pass other than 0
+    ph2 = float((w16 < 1.0).any(1).float().mean())
     print(f"iter {i}: alpha hist {hist}; 32-problem waves needing round 2 {r2:.3f}, round 3 {r3:.3f}; "
-          f"16-problem waves needing a 5th candidate {q2:.3f}", flush=True)
+          f"16-problem waves needing a 5th candidate {q2:.3f}, a phase-2 rewrite {ph2:.3f}", flush=True)
