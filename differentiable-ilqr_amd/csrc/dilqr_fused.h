@@ -1001,13 +1001,18 @@ DEV unsigned mpc_begin_lane(int T, int B, int b, const Model& md, const float* _
   return 0u;
 }
 
+// done_counter[kDenseCount]: the problems whose cost iteration 0 found not to
+// be a time-invariant diagonal one (the 16-lanes-per-problem models' dense-cost
+// instantiations have nothing to do when it is 0)
+constexpr int kDenseCount = 9;
+
 // The control words and the stop rule's sync counters of a new solve.
 DEV void mpc_reset_ctrl(const MpcState& S) {
   dilqr_mpc_ctrl z = {};
   S.ctrl[0] = z;
   S.ctrl[1] = z;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) S.done_counter[i] = 0u;
+  for (int i = 0; i <= kDenseCount; ++i) S.done_counter[i] = 0u;
 }
 
 // ---------------- a whole fixed-count solve in ONE launch (thread-per-problem

@@ -145,7 +145,7 @@ struct Group8Cost {
 // registers (its own instantiation: the caller's rows would keep 32 more
 // registers live across the step)
 template <class Model, int MODE, bool DCONST, class LdsT>
-DEV void group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Model& md,
+DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Model& md,
                       Group8Cost& cs, const float* __restrict__ x, const float* __restrict__ u, const Bounds& bd,
                       float* __restrict__ ws, float* __restrict__ cpk_out, unsigned char* __restrict__ sym_out) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
@@ -347,7 +347,9 @@ DEV void group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
       cpk_out[(size_t)b * 2 * d + d + rb] = cc_last[1];
       if (l == 0) sym_out[b] = grp ? 7 : 0;
     }
+    return !grp;                                   // iteration 0: this problem keeps the caller's cost
   }
+  return false;
 }
 
 }  // namespace dilqr

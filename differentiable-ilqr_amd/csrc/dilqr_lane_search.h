@@ -258,6 +258,8 @@ __global__ void __launch_bounds__(64) k_mpc_search_lane(int T, int B, const floa
 // k_mpc_search_lane, with one round (and at most one rewrite) where the pairs
 // took up to three rounds (max_ls = 5), two waves per SIMD at config 3 where
 // the pairs had one, and no second candidate stream to HBM.
+// the quad search's prefetch distance (0: its two waves per SIMD hide the loads)
+// and its launch-bounds floor
 #ifndef DILQR_QUAD_PFD
 #define DILQR_QUAD_PFD 0
 #endif
@@ -265,17 +267,12 @@ __global__ void __launch_bounds__(64) k_mpc_search_lane(int T, int B, const floa
 #define DILQR_QUAD_WAVES 2
 #endif
 template <class Model, int BM, bool DCONST>
-__global__ void __launch_bounds__(64, DCONST ? DILQR_QUAD_WAVES : 1) k_mpc_search_quad(int T, int B, const float* __restrict__ theta,
-                                                        const float* __restrict__ x_init,
-                                                        const float* __restrict__ C, const float* __restrict__ c,
-                                                        Bounds bd, float decay, int max_ls, int iteration,
-                                                        float best_cost_eps, int G, MpcState S) {
+DEV void search_quad_problem(int T, int B, int tid, const Model& md, const float* __restrict__ x_init,
+                             const float* __restrict__ C, const float* __restrict__ c, const Bounds& bd, float decay,
+                             int max_ls, int iteration, float best_cost_eps, const MpcState& S) {
   constexpr int n = Model::N, m = Model::M, d = n + m;
-  if (iteration > 0 && G >= 0 && S.ctrl[iteration & 1].stopped) return;
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = tid >> 2, j = tid & 3;
   if (b >= B) return;                                          // a whole quad
-  Model md; md.load(theta);
   const bool first = iteration == 0;
   const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
   const int cur = S.slot[b], best = S.slot[B + b];
@@ -342,6 +339,25 @@ __global__ void __launch_bounds__(64, DCONST ? DILQR_QUAD_WAVES : 1) k_mpc_searc
   S.improved[b] = (first || better) ? (better ? 2 : 1) : 0;
   if (S.best_iter && (first || better)) S.best_iter[b] = iteration;       // fixed-count solves
   S.slot[b] = (unsigned char)sa;
+}
+
+template <class Model, int BM, bool DCONST>
+__global__ void __launch_bounds__(64, DCONST ? DILQR_QUAD_WAVES : 1) k_mpc_search_quad(int T, int B, const float* __restrict__ theta,
+                                                        const float* __restrict__ x_init,
+                                                        const float* __restrict__ C, const float* __restrict__ c,
+                                                        Bounds bd, float decay, int max_ls, int iteration,
+                                                        float best_cost_eps, int G, MpcState S) {
+  constexpr int n = Model::N, m = Model::M, d = n + m;
+  if (iteration > 0 && G >= 0 && S.ctrl[iteration & 1].stopped) return;
+  // the dense-cost instantiation when iteration 0 found no dense cost (launched
+  // on a small grid then): nothing to do
+  if (!DCONST && S.Cpk && S.done_counter[kDenseCount] == 0u) return;
+  Model md; md.load(theta);
+  const int nq = (int)(((long long)4 * B + blockDim.x - 1) / blockDim.x);
+  for (int blk = blockIdx.x; blk < nq; blk += gridDim.x)    // one pass unless the grid is small
+    search_quad_problem<Model, BM, DCONST>(T, B, blk * blockDim.x + threadIdx.x, md, x_init, C, c, bd, decay,
+                                           max_ls, iteration, best_cost_eps, S);
+
 }
 
 }  // namespace dilqr

@@ -88,28 +88,40 @@ __global__ void __launch_bounds__(64, MODE == GAIN_BOX ? 2 : DCONST ? DILQR_SWEE
   __shared__ Group8Lds<n, m, MODE != GAIN_UNC> Ls[kG8PW];
   if (mpc_decide(S, B, iteration, G, eps, not_improved_lim)) return;
   const bool first = iteration == 0;
+  // the dense-cost instantiation after iteration 0, when iteration 0 found
+  // every cost to be a time-invariant diagonal one: nothing to do (it is
+  // launched on a small grid then, kDenseGrid8, so an empty pass costs little)
+  if (!DCONST && !first && S.Cpk && S.done_counter[kDenseCount] == 0u) return;
   const int l = threadIdx.x & (kG8 - 1), gp = threadIdx.x / kG8;
-  const int b0 = blockIdx.x * kG8PW + gp;
-  const bool valid = b0 < B;
-  const int b = valid ? b0 : B - 1;
   Model md; md.load(theta);
   const size_t TBn = (size_t)T * B * n, TBm = (size_t)T * B * m;
-  const int cur = S.slot[b];
-  // the register cost when every problem of the wave has one (wave-uniform);
-  // the two kinds of wave run in two instantiations launched back to back,
-  // each leaving the other's waves at once
-  const bool dconst = !first && S.Cpk && S.cost_sym[b] == 7;
-  if (__all(dconst) != DCONST) return;
-  Group8Cost cs{C, c, DCONST, {0.f, 0.f}, {0.f, 0.f}};
-  if (DCONST) {
+  const int nblk = (B + kG8PW - 1) / kG8PW;
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {   // one pass unless the grid is small
+    const int b0 = blk * kG8PW + gp;
+    const bool valid = b0 < B;
+    const int b = valid ? b0 : B - 1;
+    const int cur = S.slot[b];
+    // the register cost when every problem of the wave has one (wave-uniform);
+    // the two kinds of wave run in two instantiations launched back to back,
+    // each leaving the other's waves at once
+    const bool dconst = !first && S.Cpk && S.cost_sym[b] == 7;
+    if (__all(dconst) != DCONST) continue;
+    Group8Cost cs{C, c, DCONST, {0.f, 0.f}, {0.f, 0.f}};
+    if (DCONST) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      cs.cd[k] = S.Cpk[(size_t)b * 2 * d + l + kG8 * k];        // rows l, l + 8
-      cs.cc[k] = S.Cpk[(size_t)b * 2 * d + d + l + kG8 * k];
+      for (int k = 0; k < 2; ++k) {
+        cs.cd[k] = S.Cpk[(size_t)b * 2 * d + l + kG8 * k];        // rows l, l + 8
+        cs.cc[k] = S.Cpk[(size_t)b * 2 * d + d + l + kG8 * k];
+      }
+    }
+    const bool dense = group8_sweep<Model, MODE, DCONST>(Ls[gp], T, B, b, l, valid, md, cs, S.Xs + cur * TBn,
+                                                         S.Us + cur * TBm, bd, S.ws, first ? S.Cpk : nullptr,
+                                                         first ? S.cost_sym : nullptr);
+    if (!DCONST && first && S.Cpk) {                              // count the problems that stay dense
+      const unsigned long long bal = __ballot(dense && valid && l == 0);
+      if ((threadIdx.x & 63) == 0 && bal) atomicAdd(&S.done_counter[kDenseCount], (unsigned)__popcll(bal));
     }
   }
-  group8_sweep<Model, MODE, DCONST>(Ls[gp], T, B, b, l, valid, md, cs, S.Xs + cur * TBn, S.Us + cur * TBm, bd, S.ws,
-                            first ? S.Cpk : nullptr, first ? S.cost_sym : nullptr);
 }
 
 // DILQR_SWEEP_LANES: 8 (default) or 16 lanes per problem in the MPC sweep (the
@@ -117,6 +129,12 @@ __global__ void __launch_bounds__(64, MODE == GAIN_BOX ? 2 : DCONST ? DILQR_SWEE
 #ifndef DILQR_SWEEP_LANES
 #define DILQR_SWEEP_LANES 8
 #endif
+// workgroups of a dense-cost launch that usually finds nothing to do
+#ifndef DILQR_DENSE_GRID
+#define DILQR_DENSE_GRID 256
+#endif
+constexpr int kDenseGrid = DILQR_DENSE_GRID;
+
 // DILQR_SEARCH_QUAD: the line search on a quad of lanes per problem (1, the
 // default: every pass of a round at once, cost only) or on lane pairs (0)
 #ifndef DILQR_SEARCH_QUAD
@@ -124,8 +142,10 @@ __global__ void __launch_bounds__(64, MODE == GAIN_BOX ? 2 : DCONST ? DILQR_SWEE
 #endif
 int launch_mpc_step_rocket(const MpcStepArgs& a) {
 #if DILQR_SEARCH_QUAD
+  const int gq = grid_for(4 * (long long)a.B);
+  const int gq_dense = a.st.Cpk ? (gq < kDenseGrid ? gq : kDenseGrid) : gq;
 #define SEARCH(BM_, DC_)                                                                                          \
-  k_mpc_search_quad<Rocket, BM_, DC_><<<grid_for(4 * (long long)a.B), kBlock, 0, a.stream>>>(                     \
+  k_mpc_search_quad<Rocket, BM_, DC_><<<DC_ ? gq : gq_dense, kBlock, 0, a.stream>>>(                             \
       a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st)
 #else
 #define SEARCH(BM_, DC_)                                                                                          \
@@ -133,13 +153,22 @@ int launch_mpc_step_rocket(const MpcStepArgs& a) {
       a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st)
 #endif
 #if DILQR_SWEEP_LANES == 8
+  // the dense-cost instantiations after iteration 0 (with a packed copy):
+  // a small grid that strides over the problems, so that the usual empty pass
+  // (every cost a time-invariant diagonal one) costs a few workgroups, not
+  // B/8 of them
+  const int g8 = (int)((a.B + kG8PW - 1) / kG8PW);
+  const int g8_dense = (a.iteration > 0 && a.st.Cpk) ? (g8 < kDenseGrid ? g8 : kDenseGrid) : g8;
 #define SWEEP8(MODE_, DC_)                                                                                        \
-  k_mpc_sweep_g8<Rocket, MODE_, DC_><<<(int)((a.B + kG8PW - 1) / kG8PW), 64, 0, a.stream>>>(                     \
+  k_mpc_sweep_g8<Rocket, MODE_, DC_><<<DC_ ? g8 : g8_dense, 64, 0, a.stream>>>(                                   \
       a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st)
 #define SWEEP(MODE_)                                                                                              \
   SWEEP8(MODE_, true);                                                                                            \
   SWEEP8(MODE_, false)
 #else
+#if DILQR_SEARCH_QUAD
+#error "the quad search relies on the 8-lane sweep's count of dense-cost problems (kDenseCount)"
+#endif
 #define SWEEP(MODE_)                                                                                              \
   k_mpc_sweep_group<Rocket, MODE_><<<grid_group(a.B), 64, 0, a.stream>>>(                                         \
       a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st)
