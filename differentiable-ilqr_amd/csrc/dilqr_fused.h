@@ -1094,6 +1094,113 @@ __global__ void __launch_bounds__(kBlock, DILQR_SOLVE_OCC) k_mpc_solve_fixed(int
   DILQR_STAMP(7);
 }
 
+// ---------------- a whole stop-rule solve in ONE launch for a small batch
+// (B <= kSmallMax: the IL loop's n_batch = 32, il_exp.py:44).  The stop rule
+// (mpc_explicit.py:264-299) couples the batch only through the quirk rows of
+// full_du_norm and two reductions (max row norm, "any improved"); with every
+// problem in one workgroup those are a barrier and an LDS reduction, so the
+// loop needs no launch per iteration and no host poll.  Each lane runs the
+// same per-lane code as k_mpc_solve_fixed (begin, iteration 0 without PREV,
+// then PREV), and after each iteration the workgroup forms the rows exactly as
+// k_mpc_norm_rows does (same order of summation) and applies the rule exactly
+// as mpc_decide does: the same iterates, costs, best_du, full_du_norm and
+// stop iteration as the per-iteration launches
+// (test_small_batch_solve_equals_per_iteration_launches).
+constexpr int kSmallMax = 1024;
+
+template <class Model, int BM, bool LG>
+__global__ void __launch_bounds__(kSmallMax) k_mpc_solve_small(int T, int B, const float* __restrict__ theta,
+                                                               const float* __restrict__ x_init,
+                                                               const float* __restrict__ u_init,
+                                                               const float* __restrict__ C,
+                                                               const float* __restrict__ c, Bounds bd, float decay,
+                                                               int max_ls, int iters, float best_cost_eps, float eps,
+                                                               int not_improved_lim, MpcState S) {
+  constexpr int m = Model::M;
+  __shared__ unsigned red_max[kSmallMax / 64];
+  __shared__ int red_any[kSmallMax / 64];
+  extern __shared__ __attribute__((aligned(16))) float lds_gains[];
+  const int b = threadIdx.x;
+  const bool act = b < B;
+  const int nw = (int)(blockDim.x + 63) / 64, w = b >> 6;
+  const int TM = T * m;
+  Model md; md.load(theta);
+  unsigned pk = 0u;
+  LaneIter r{0.f, 0.f, 0};
+  int cur = 0, best = 0, imp = 0;
+  float best_cost = 0.f;
+  if (act) {
+    pk = S.Cpk ? mpc_begin_lane<Model, true>(T, B, b, md, x_init, u_init, S, C, c)
+               : mpc_begin_lane<Model>(T, B, b, md, x_init, u_init, S);
+    r = mpc_iteration_lane<Model, BM, LG, false, false, 64>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
+                                                            S.du_sq, lds_gains, 0, 0, pk, 0.f);
+    cur = best = r.slot;
+    best_cost = r.cost;
+    imp = 1;
+  }
+  int done = 0, n_not_improved = 0, stopped = 0;
+  unsigned mx_all = 0u;
+  for (;;) {
+    ++done;
+    __syncthreads();                                       // every lane's du rows of this iteration are stored
+    unsigned mx = 0u;
+    int any = 0;
+    if (act) {                                             // k_mpc_norm_rows, row b
+      float s2 = 0.f;
+      const float* p = S.du_sq + (size_t)b * TM;
+      for (int i = 0; i < TM; ++i) s2 += p[i];
+      const float fdn = sqrtf(s2);
+      S.full_du_norm[b] = fdn;
+      if (imp) S.best_du[b] = fdn;
+      mx = __float_as_uint(fdn);
+      any = imp == 2;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned o = __shfl_xor(mx, off, 64);
+      mx = o > mx ? o : mx;
+      any |= __shfl_xor(any, off, 64);
+    }
+    if ((b & 63) == 0) { red_max[w] = mx; red_any[w] = any; }
+    __syncthreads();                                       // (also: every lane has read its row)
+    mx = 0u;
+    any = 0;
+    for (int i = 0; i < nw; ++i) { mx = red_max[i] > mx ? red_max[i] : mx; any |= red_any[i]; }
+    mx_all = mx;
+    if (done == iters) break;                              // the last iteration's rule is never applied
+    n_not_improved = any ? 0 : n_not_improved + 1;         // mpc_explicit.py:264, 279 (mpc_decide)
+    if (__uint_as_float(mx) < eps || n_not_improved > not_improved_lim) {   // 297-299
+      stopped = 1;
+      break;
+    }
+    if (act) {
+      r = mpc_iteration_lane<Model, BM, LG, false, true, 64>(T, B, b, md, x_init, C, c, bd, decay, max_ls, S,
+                                                             S.du_sq, lds_gains, cur, best, pk, r.cost);
+      const bool take = mpc_takes_best(false, r.cost, best_cost, best_cost_eps);
+      if (take) { best_cost = r.cost; best = r.slot; }
+      imp = take ? 2 : 0;
+      cur = r.slot;
+    }
+  }
+  if (act) {                                               // the state the per-iteration launches leave
+    S.cost[b] = r.cost;
+    S.alpha[b] = r.alpha;
+    S.best_cost[b] = best_cost;
+    S.slot[b] = (unsigned char)cur;
+    S.slot[B + b] = (unsigned char)best;
+    S.improved[b] = imp;
+  }
+  if (b == 0) {
+    dilqr_mpc_ctrl o = {};
+    o.iter = done;
+    o.stopped = stopped;
+    o.n_not_improved = n_not_improved;
+    o.max_du_bits = mx_all;
+    S.ctrl[0] = o;
+    S.ctrl[1] = o;
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 // Gain records in LDS (lds bytes per 64-problem workgroup) when four
 // workgroups per CU fit — one wave per SIMD at the headline's 65536 problems —
@@ -1156,6 +1263,32 @@ int launch_mpc_solve_tpp(const MpcSolveArgs& a) {
   else if (a.bd.mode != DILQR_BOUNDS_NONE) LAUNCH_SOLVE(DILQR_BOUNDS_SCALAR);
   else LAUNCH_SOLVE(DILQR_BOUNDS_NONE);
 #undef LAUNCH_SOLVE
+  return launched();
+}
+
+// a whole stop-rule solve of one thread-per-problem model in one workgroup
+// (B <= kSmallMax; gain records in LDS for one wave when they fit)
+template <class MD>
+int launch_mpc_solve_small_tpp(const MpcSolveArgs& a, float eps, int lim) {
+  if (a.B > kSmallMax) return DILQR_E_SHAPE;
+  const int threads = (a.B + 63) / 64 * 64;
+  const size_t lds = (size_t)a.T * 64 * (MD::N * MD::M + MD::M) * sizeof(float);
+  const bool lg = threads == 64 && lds <= 65536 && !kNoLdsGains;
+#define LAUNCH_SMALL(BM_)                                                                                    \
+  do {                                                                                                       \
+    if (lg)                                                                                                  \
+      k_mpc_solve_small<MD, BM_, true><<<1, threads, lds, a.stream>>>(                                        \
+          a.T, a.B, a.theta, a.x_init, a.u_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iters, a.best_cost_eps, eps, \
+          lim, a.st);                                                                                        \
+    else                                                                                                     \
+      k_mpc_solve_small<MD, BM_, false><<<1, threads, 0, a.stream>>>(                                         \
+          a.T, a.B, a.theta, a.x_init, a.u_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iters, a.best_cost_eps, eps, \
+          lim, a.st);                                                                                        \
+  } while (0)
+  if (a.bd.mode == DILQR_BOUNDS_TENSOR) LAUNCH_SMALL(DILQR_BOUNDS_TENSOR);
+  else if (a.bd.mode != DILQR_BOUNDS_NONE) LAUNCH_SMALL(DILQR_BOUNDS_SCALAR);
+  else LAUNCH_SMALL(DILQR_BOUNDS_NONE);
+#undef LAUNCH_SMALL
   return launched();
 }
 

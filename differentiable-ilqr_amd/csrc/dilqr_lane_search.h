@@ -347,7 +347,6 @@ __global__ void __launch_bounds__(64, DCONST ? DILQR_QUAD_WAVES : 1) k_mpc_searc
                                                         const float* __restrict__ C, const float* __restrict__ c,
                                                         Bounds bd, float decay, int max_ls, int iteration,
                                                         float best_cost_eps, int G, MpcState S) {
-  constexpr int n = Model::N, m = Model::M, d = n + m;
   if (iteration > 0 && G >= 0 && S.ctrl[iteration & 1].stopped) return;
   // the dense-cost instantiation when iteration 0 found no dense cost (launched
   // on a small grid then): nothing to do

@@ -54,6 +54,9 @@ int launch_mpc_step_pendulum_complex(const MpcStepArgs& a);
 int launch_mpc_solve_pendulum(const MpcSolveArgs& a);
 int launch_mpc_solve_cartpole(const MpcSolveArgs& a);
 int launch_mpc_solve_pendulum_complex(const MpcSolveArgs& a);
+int launch_mpc_solve_small_pendulum(const MpcSolveArgs& a, float eps, int lim);
+int launch_mpc_solve_small_cartpole(const MpcSolveArgs& a, float eps, int lim);
+int launch_mpc_solve_small_pendulum_complex(const MpcSolveArgs& a, float eps, int lim);
 int launch_ilqr_iterate_pendulum(const IlqrIterArgs& a);
 int launch_ilqr_iterate_cartpole(const IlqrIterArgs& a);
 int launch_ilqr_iterate_rocket(const IlqrIterArgs& a);

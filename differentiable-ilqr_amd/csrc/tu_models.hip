@@ -205,7 +205,7 @@ using namespace dilqr;
 
 extern "C" {
 
-int dilqr_version(void) { return 8; }
+int dilqr_version(void) { return 9; }
 
 // hash of csrc/ + include/dilqr.h at build time (Makefile); _native checks it
 // against the tree so a stale prebuilt library cannot be loaded silently

@@ -364,6 +364,25 @@ int dilqr_mpc_solve_fixed_f32(int model, int T, int B, const float* theta, const
   return dilqr_mpc_finish_fixed_f32(T, m, B, iterations, st, stream);
 }
 
+int dilqr_mpc_solve_small_f32(int model, int T, int B, const float* theta, const float* x_init, const float* u_init,
+                              const float* C, const float* c, dilqr_bounds bounds, float linesearch_decay,
+                              int max_linesearch_iter, int iterations, float best_cost_eps, float eps,
+                              int not_improved_lim, dilqr_mpc_state st, void* stream) {
+  if (T < 1 || B < 0 || max_linesearch_iter < 1 || iterations < 1 || !theta || !x_init || !C || !c) return DILQR_E_ARG;
+  if (!al16(x_init) || !al16(C) || !al16(c) || bad_state(st) || bad_bounds(bounds)) return DILQR_E_ARG;
+  if (u_init && ((uintptr_t)u_init & 3u)) return DILQR_E_ARG;
+  if (B > kSmallMax) return DILQR_E_SHAPE;
+  if (B == 0) return 0;
+  const MpcSolveArgs a{T, B, theta, x_init, u_init, C, c, mkb(bounds), linesearch_decay, max_linesearch_iter,
+                       iterations, best_cost_eps, st, S(stream)};
+  switch (model) {
+    case DILQR_MODEL_PENDULUM: return launch_mpc_solve_small_pendulum(a, eps, not_improved_lim);
+    case DILQR_MODEL_CARTPOLE: return launch_mpc_solve_small_cartpole(a, eps, not_improved_lim);
+    case DILQR_MODEL_PENDULUM_COMPLEX: return launch_mpc_solve_small_pendulum_complex(a, eps, not_improved_lim);
+    default: return DILQR_E_SHAPE;            // rocket: its sweep and search use different lane mappings
+  }
+}
+
 int dilqr_mpc_stop_rule_f32(int T, int m, int B, int iteration, dilqr_mpc_state st, void* stream) {
   if (T < 1 || m < 1 || B < 0 || iteration < 0 || bad_state(st)) return DILQR_E_ARG;
   if (B == 0) return 0;

@@ -6,6 +6,9 @@ namespace dilqr {
 int launch_mpc_step_cartpole(const MpcStepArgs& a) { return launch_mpc_step_tpp<Cartpole>(a); }
 int launch_ilqr_iterate_cartpole(const IlqrIterArgs& a) { return launch_ilqr_iterate_tpp<Cartpole>(a); }
 int launch_mpc_solve_cartpole(const MpcSolveArgs& a) { return launch_mpc_solve_tpp<Cartpole>(a); }
+int launch_mpc_solve_small_cartpole(const MpcSolveArgs& a, float eps, int lim) {
+  return launch_mpc_solve_small_tpp<Cartpole>(a, eps, lim);
+}
 }  // namespace dilqr
 
 #ifdef DILQR_STAMPS

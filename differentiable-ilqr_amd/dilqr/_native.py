@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must be imported first: libdilqr.so then binds to t
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DILQR_LIB", os.path.join(_HERE, "libdilqr.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 _PKG = os.path.dirname(_HERE)          # differentiable-ilqr_amd/ (the Makefile's directory)
 
 MODEL_LINDX, MODEL_PENDULUM, MODEL_CARTPOLE, MODEL_ROCKET, MODEL_PENDULUM_COMPLEX = 0, 1, 2, 3, 4
@@ -72,6 +72,8 @@ SIGNATURES = {
     "dilqr_mpc_finish_fixed_f32": ([_i, _i, _i, _i, MpcState, _vp], _i),
     "dilqr_mpc_solve_fixed_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, MpcState, _vp],
                                   _i),
+    "dilqr_mpc_solve_small_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, Bounds, _f, _i, _i, _f, _f, _i, MpcState,
+                                   _vp], _i),
     "dilqr_mpc_gather_best_f32": ([_i, _i, _i, _i, MpcState, _vp, _vp, _vp], _i),
     "dilqr_get_matrices_f32": ([_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dilqr_grad_input_f32": ([_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

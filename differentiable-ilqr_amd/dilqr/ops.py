@@ -294,6 +294,20 @@ class MPCSolve:
         self._u0 = u0
         self.last_iteration = self.fixed_iters - 1
 
+    def solve_small(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, iterations, best_cost_eps, eps,
+                    not_improved_lim, u_init=None):
+        """A whole stop-rule solve in one launch (dilqr_mpc_solve_small_f32: B <=
+        SMALL_BATCH_MAX, one workgroup, the rule applied in-kernel after each
+        iteration); the same bits as begin + iterate per iteration."""
+        u0 = self._u_init(u_init)
+        N.call("dilqr_mpc_solve_small_f32", model_id, self.T, self.B, N.ptr(theta), N.ptr(x_init),
+               None if u0 is None else N.ptr(u0), N.ptr(C), N.ptr(c), bounds, float(decay), int(max_ls),
+               int(iterations), float(best_cost_eps), float(eps), int(min(not_improved_lim, 2 ** 31 - 1)),
+               self.state, N.stream(x_init.device))
+        self._u0 = u0
+        self.small = True
+        self.last_iteration = iterations - 1
+
     def iterate(self, model_id, theta, x_init, C, c, bounds, decay, max_ls, iteration, best_cost_eps, eps,
                 not_improved_lim):
         """Iteration `iteration` (0, 1, ...) of the solve started by begin()."""
@@ -330,7 +344,7 @@ class MPCSolve:
 
     def _ctrl_now(self):
         k = max(self.last_iteration, 0)
-        return self.ctrl.view(2, N.CTRL_INTS)[k & 1]
+        return self.ctrl.view(2, N.CTRL_INTS)[k & 1]        # solve_small writes both words
 
     def gather_best(self):
         x = torch.empty(self.T, self.B, self.n, device=self.Xs.device)
@@ -348,6 +362,11 @@ class MPCSolve:
     @property
     def iterations(self):
         return int(self._ctrl_now()[0].item())
+
+
+# dilqr_mpc_solve_small_f32: batches one workgroup holds, thread-per-problem models
+SMALL_BATCH_MAX = 1024
+SMALL_BATCH_MODELS = (N.MODEL_PENDULUM, N.MODEL_CARTPOLE, N.MODEL_PENDULUM_COMPLEX)
 
 
 def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upper=None, lqr_iter=10,
@@ -384,6 +403,13 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
     if fixed:
         sv.solve_fixed(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, best_cost_eps,
                        u_init)
+        del keep
+        x, u = sv.gather_best()
+        return x, u, sv.best_cost, sv.best_du, sv
+    if B <= SMALL_BATCH_MAX and model_id in SMALL_BATCH_MODELS and lqr_iter >= 1:
+        # the whole stop-rule loop in one launch (one workgroup holds the batch)
+        sv.solve_small(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, lqr_iter,
+                       best_cost_eps, eps, not_improved_lim, u_init)
         del keep
         x, u = sv.gather_best()
         return x, u, sv.best_cost, sv.best_du, sv

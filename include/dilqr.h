@@ -376,6 +376,24 @@ int dilqr_mpc_solve_fixed_f32(int model, int T, int B, const float* theta, const
                               int max_linesearch_iter, int iterations, float best_cost_eps,
                               dilqr_mpc_state st, void* stream);
 
+/* A whole stop-rule solve in one launch for a small batch (ABI 9): begin (u_init
+   as in dilqr_mpc_begin_f32), then up to `iterations` iterations with the stop
+   rule (mpc_explicit.py:264-299: max full_du_norm < eps or n_not_improved >
+   not_improved_lim) applied after each, inside ONE workgroup holding every
+   problem — the rule's batch-mixing rows and reductions need a barrier, not a
+   launch, and the host polls nothing.  The same iterates, costs, best_du,
+   full_du_norm and stop iteration as dilqr_mpc_begin_f32 +
+   dilqr_mpc_iterate_f32 per iteration; ctrl[0] = ctrl[1] = {iterations run,
+   stopped, n_not_improved, max_du_bits}.  B <= 1024 and the thread-per-problem
+   models (pendulum, cartpole, 5-parameter pendulum); DILQR_E_SHAPE otherwise.
+   Replaces the per-iteration loop of MPC.forward for the IL loop's batches
+   (il_exp.py:44 n_batch = 32, il_env.py:153-188). */
+int dilqr_mpc_solve_small_f32(int model, int T, int B, const float* theta, const float* x_init,
+                              const float* u_init, const float* C, const float* c,
+                              dilqr_bounds bounds, float linesearch_decay,
+                              int max_linesearch_iter, int iterations, float best_cost_eps,
+                              float eps, int not_improved_lim, dilqr_mpc_state st, void* stream);
+
 /* Materialise each problem's best trajectory into x_out [T,B,n], u_out [T,B,m]. */
 int dilqr_mpc_gather_best_f32(int n, int m, int T, int B, dilqr_mpc_state st, float* x_out,
                               float* u_out, void* stream);

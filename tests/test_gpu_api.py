@@ -185,3 +185,57 @@ def test_qp_total_vs_golden_and_per_step_maxima(golden, name, n, m):
     print(f"{name}: qp_total {total}, per-problem oracle {o_total}, reference {ref}")
     assert total == o_total
     assert total == ref
+
+
+@pytest.mark.parametrize("model,B,bounds,eps,lim", [
+    ("cartpole", 32, (-100.0, 100.0), 1e-4, 5),       # the IL loop's settings (il_env.py:153-188), n_batch 32
+    ("cartpole", 100, None, 5e-2, 5),                 # stops on max full_du_norm < eps
+    ("cartpole", 1024, (-10.0, 10.0), 1e-3, 1),       # one full workgroup; n_not_improved > 1 can stop it
+    ("pendulum", 77, (-2.0, 2.0), 1e-3, 5),
+    ("cartpole", 64, None, 0.0, 3),                   # eps 0: only the not-improved rule
+])
+def test_small_batch_solve_equals_per_iteration_launches(model, B, bounds, eps, lim):
+    """dilqr_mpc_solve_small_f32 (the whole stop-rule loop in ONE workgroup,
+    the rule applied in-kernel) leaves exactly the state of begin + the
+    per-iteration launches (fused iteration + k_mpc_norm_rows + the next
+    prologue's mpc_decide): best trajectories, costs, best_du, full_du_norm,
+    step sizes, slots and the iteration the rule stopped at."""
+    from dilqr import _native as N
+    from dilqr import ops
+    from dilqr.env_dx.cartpole import CartpoleDx
+    from dilqr.env_dx.pendulum import PendulumDx
+    T, iters = (35, 60) if model == "cartpole" else (20, 60)
+    dx = CartpoleDx() if model == "cartpole" else PendulumDx()
+    rng = np.random.RandomState(B)
+    if model == "cartpole":
+        th = rng.uniform(-np.pi, np.pi, B)
+        x0 = np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                       rng.uniform(-1, 1, B)], 1)
+        decay, mls = 0.5, 2
+    else:
+        th = rng.uniform(-np.pi / 2, np.pi / 2, B)
+        x0 = np.stack([np.cos(th), np.sin(th), rng.uniform(-1, 1, B)], 1)
+        decay, mls = 0.2, 5
+    x0 = torch.tensor(x0, dtype=torch.float32, device=DEV)
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV).contiguous()
+    c = p.repeat(T, B, 1).to(DEV).contiguous()
+    th_ = ops.theta_of(dx, x0)
+    n, m = dx.n_state, dx.n_ctrl
+    nb, keep = N.make_bounds(*(bounds if bounds else (None, None)))
+    a = ops.MPCSolve(T, B, n, m, DEV)
+    a.solve_small(dx.model_id, th_, x0, C, c, nb, decay, mls, iters, 1e-4, eps, lim)
+    b = ops.MPCSolve(T, B, n, m, DEV)
+    b.begin(dx.model_id, th_, x0)
+    for i in range(iters):
+        b.iterate(dx.model_id, th_, x0, C, c, nb, decay, mls, i, 1e-4, eps, lim)
+    ran_b = b.iterations if b.stopped else iters
+    print(f"{model} B={B}: small solve ran {a.iterations} (stopped {a.stopped}), per-iteration {ran_b} "
+          f"(stopped {b.stopped})")
+    assert a.iterations == ran_b and a.stopped == b.stopped
+    xa, ua = a.gather_best()
+    xb, ub = b.gather_best()
+    assert torch.equal(xa, xb) and torch.equal(ua, ub)
+    for f in ("best_cost", "best_du", "full_du_norm", "cost", "alpha", "slot", "improved"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    del keep

@@ -1207,22 +1207,26 @@ def test_implicit_backward_u_zero_I_vs_golden(golden):
     assert max(errs) < 1e-4
 
 
-def test_rocket_register_cost_bit_identical():
+@pytest.mark.parametrize("B,off", [(64, 40), (12288, 12256)])
+def test_rocket_register_cost_bit_identical(B, off):
     """The 16-lane MPC kernel holds a time-invariant diagonal cost in two
     registers per lane (flag 7 from iteration 0) instead of reading the caller's
     16 x 16 rows every step and pass: the same values, so bit-identical
     trajectories and costs with and without the solve's cost record, on a batch
-    that mixes flagged problems with a time-varying and a non-diagonal cost."""
+    that mixes flagged problems with a time-varying and a non-diagonal cost.
+    At B = 12288 the dense problems are the batch's last: after iteration 0 the
+    dense-cost sweep and search run on a small grid striding over the batch
+    (kDenseGrid workgroups), which must reach them."""
     from dilqr import _native as N
     from dilqr import ops
     dx = dilqr_models()["rocket"]()
-    T, B, n, m = 12, 64, 13, 3
+    T, n, m = 12, 13, 3
     q, p = dx.get_true_obj()
     C = torch.diag(q).repeat(T, B, 1, 1)
     c = p.repeat(T, B, 1).clone()
-    C[:, 40:48, 0, 1] += 1e-3                     # not diagonal
-    C[:, 40:48, 1, 0] += 1e-3
-    c[3, 48:56] += 0.01                           # not time-invariant
+    C[:, off:off + 8, 0, 1] += 1e-3               # not diagonal
+    C[:, off:off + 8, 1, 0] += 1e-3
+    c[3, off + 8:off + 16] += 0.01                # not time-invariant
     C, c = C.to(DEV).contiguous(), c.to(DEV).contiguous()
     x0 = gpu(rocket_x0(B, seed=4))
     theta = ops.theta_of(dx, x0)
@@ -1237,6 +1241,6 @@ def test_rocket_register_cost_bit_identical():
         out.append((x, u, sv.best_cost.clone()))
         if packed:
             flags = cpu(sv.cost_sym)
-            assert (flags[:40] == 7).all() and (flags[56:] == 7).all() and (flags[40:56] == 0).all()
+            assert (flags[:off] == 7).all() and (flags[off + 16:] == 7).all() and (flags[off:off + 16] == 0).all()
     for a, b in zip(*out):
         assert same_bits(a, b)
