@@ -1106,7 +1106,11 @@ __global__ void __launch_bounds__(kBlock, DILQR_SOLVE_OCC) k_mpc_solve_fixed(int
 // as mpc_decide does: the same iterates, costs, best_du, full_du_norm and
 // stop iteration as the per-iteration launches
 // (test_small_batch_solve_equals_per_iteration_launches).
-constexpr int kSmallMax = 1024;
+// (256: four waves, one per SIMD of the CU — a larger workgroup would bound the
+// per-lane iteration's registers at 512 / waves-per-SIMD and spill it; the first
+// build at 1024 threads ran the IL step at B = 32 in 7.8 ms against 6.3 ms for
+// the per-iteration launches)
+constexpr int kSmallMax = 256;
 
 template <class Model, int BM, bool LG>
 __global__ void __launch_bounds__(kSmallMax) k_mpc_solve_small(int T, int B, const float* __restrict__ theta,

@@ -365,7 +365,7 @@ class MPCSolve:
 
 
 # dilqr_mpc_solve_small_f32: batches one workgroup holds, thread-per-problem models
-SMALL_BATCH_MAX = 1024
+SMALL_BATCH_MAX = 256
 SMALL_BATCH_MODELS = (N.MODEL_PENDULUM, N.MODEL_CARTPOLE, N.MODEL_PENDULUM_COMPLEX)
 
 

@@ -384,7 +384,7 @@ int dilqr_mpc_solve_fixed_f32(int model, int T, int B, const float* theta, const
    launch, and the host polls nothing.  The same iterates, costs, best_du,
    full_du_norm and stop iteration as dilqr_mpc_begin_f32 +
    dilqr_mpc_iterate_f32 per iteration; ctrl[0] = ctrl[1] = {iterations run,
-   stopped, n_not_improved, max_du_bits}.  B <= 1024 and the thread-per-problem
+   stopped, n_not_improved, max_du_bits}.  B <= 256 and the thread-per-problem
    models (pendulum, cartpole, 5-parameter pendulum); DILQR_E_SHAPE otherwise.
    Replaces the per-iteration loop of MPC.forward for the IL loop's batches
    (il_exp.py:44 n_batch = 32, il_env.py:153-188). */

@@ -53,7 +53,7 @@ def measure(B, reps=5, dev=torch.device("cuda", 0)):
             iters.append(sv.iterations if sv.stopped else sv.last_iteration + 1)
     med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
     return {"batch": B, "ms_per_step": med(tot), "forward_ms": med(fwd), "backward_ms": med(bwd),
-            "iterations": iters, "path": getattr(m.last_solve, "path", "per-iteration launches")}
+            "iterations": iters, "path": "one-launch small-batch solve" if getattr(m.last_solve, "small", False) else "per-iteration launches"}
 
 
 if __name__ == "__main__":
