@@ -295,6 +295,7 @@ constexpr int kPF = DILQR_PF;
 #define DILQR_PF_LS 1
 #endif
 constexpr int kPFL = DILQR_PF_LS;                   // the line search's prefetch distance
+static_assert(kPFL == 1, "the line search prefetches one step ahead");
 
 // ---------------- forward: the line search (lqr_step_explicit.py:166-263).
 // Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
@@ -332,7 +333,13 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
   // slower on MI355X: unrolling the step loop twice over two prefetch buffers
   // and making every store unconditional, +3 us per iteration; unrolling it
   // three times with the three prefetch buffers rotating roles instead of
-  // being copied — 13 fewer v_mov per step in the listing — +4 us.)
+  // being copied — 13 fewer v_mov per step in the listing — +4 us.  Round 5,
+  // after peeling step T-1 (1.759e9 -> 1.790e9 problem-iterations/s on one
+  // box): the loop unrolled twice over two buffers swapping roles, 172 -> 158
+  // VALU per step, no faster (1.781e9 vs 1.786e9); each candidate record
+  // stored dword by dword from the packed pairs' halves, 12 fewer v_mov per
+  // step, 9 % slower (1.60e9) — six narrow stores per record cost more than
+  // the moves they save.)
   for (int p = 0; p < max_ls; p += 2) {
     const bool twoB = p + 1 < max_ls;                       // uniform
     const float aA = alpha, aB = alpha * decay;
@@ -351,25 +358,28 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
     f2 cp = {0.f, 0.f};
     // step s's record holds x_{s+1} of the current trajectory; indices clamp at T-1
     auto cl = [T](int s) { return s < T ? s : T - 1; };
-    FwdIn<n, m, GREC, TL, BM> cur, n1, n2;
+    FwdIn<n, m, GREC, TL, BM> cur, n1;
     cur.load(ws, u, cs, x, bd, T, 0, cl(1), B, b);
     if constexpr (TL == TRAJ_REC) {                     // u_0 from record 0
       float x0r[n];
       ld_xu<TL>(x0r, cur.u, x, u, 0, B, b);
     }
-    if constexpr (kPFL >= 2) n1.load(ws, u, cs, x, bd, T, cl(1), cl(2), B, b);
-    for (int t = 0; t < T; ++t) {
-      if constexpr (kPFL >= 2) n2.load(ws, u, cs, x, bd, T, cl(t + 2), cl(t + 3), B, b);   // prefetch step t+2
-      else n1.load(ws, u, cs, x, bd, T, cl(t + 1), cl(t + 2), B, b);                      // prefetch step t+1
+    // step T-1 is peeled off the loop (LAST: no prefetch, no dynamics step), so
+    // the loop body updates the candidate states unconditionally — no branch
+    // whose join needs the old states copied into the new ones' registers
+    // c: this step's inputs, nx: the next step's, loaded here (prefetch 1)
+    auto step = [&](int t, auto last_c, auto& c, auto& nx) {
+      constexpr bool LAST = decltype(last_c)::value;
+      if constexpr (!LAST) nx.load(ws, u, cs, x, bd, T, t + 1, cl(t + 2), B, b);      // prefetch step t+1
       f2 nu[m];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
         f2 sp = {0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < n; ++j) sp += cur.g[a * n + j] * dp[j];
-        nu[a] = (sp + cur.u[a]) + al * cur.g[m * n + a];
+        for (int j = 0; j < n; ++j) sp += c.g[a * n + j] * dp[j];
+        nu[a] = (sp + c.u[a]) + al * c.g[m * n + a];
         if constexpr (BM != DILQR_BOUNDS_NONE) {
-          const float lo = cur.bnd.l(bd, a), hi = cur.bnd.h(bd, a);
+          const float lo = c.bnd.l(bd, a), hi = c.bnd.h(bd, a);
           nu[a] = f2{eclamp(nu[a].x, lo, hi), eclamp(nu[a].y, lo, hi)};
         }
       }
@@ -402,7 +412,7 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
       if (p == 0) {
 #pragma unroll
         for (int a = 0; a < m; ++a) {
-          float e = cur.u[a] - nu[a].x;
+          float e = c.u[a] - nu[a].x;
           du_sq[((size_t)t * m + a) * B + b] = e * e;
         }
       }
@@ -411,14 +421,14 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
       for (int i = 0; i < n; ++i) tau[i] = xp[i];
 #pragma unroll
       for (int a = 0; a < m; ++a) tau[n + a] = nu[a];
-      cp += quad_cost<d, CostT::kDiag>(cur.C, cur.c, tau);
-      if (t < T - 1) {
+      cp += quad_cost<d, CostT::kDiag>(c.C, c.c, tau);
+      if constexpr (!LAST) {
         f2 xnext[n];
         md.forward(xp, nu, xnext);
         float xa[n], xb[n];
 #pragma unroll
         for (int i = 0; i < n; ++i) {
-          dp[i] = xnext[i] - cur.xnext[i];
+          dp[i] = xnext[i] - c.xnext[i];
           xp[i] = xnext[i];
           xa[i] = xnext[i].x;
           xb[i] = xnext[i].y;
@@ -428,13 +438,18 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
           if (twoB) st(xb_out + ((size_t)(t + 1) * B + b) * n, xb);
         }
       }
-      if constexpr (TL == TRAJ_REC) {
+      if constexpr (!LAST) {
+        if constexpr (TL == TRAJ_REC) {
 #pragma unroll
-        for (int a = 0; a < m; ++a) n1.u[a] = cur.unext[a];     // u_{t+1}
+          for (int a = 0; a < m; ++a) nx.u[a] = c.unext[a];     // u_{t+1}
+        }
       }
+    };
+    for (int t = 0; t < T - 1; ++t) {
+      step(t, std::false_type{}, cur, n1);
       cur = n1;
-      if constexpr (kPFL >= 2) n1 = n2;
     }
+    step(T - 1, std::true_type{}, cur, n1);
     const float cA = cp.x, cB = cp.y;
     if (!(cA > old_cost) || p == max_ls - 1) { cost = cA; alpha = aA; win = 0; break; }
     if (!(cB > old_cost) || p + 1 == max_ls - 1) { cost = cB; alpha = aB; win = 1; break; }
