@@ -523,32 +523,49 @@ def secondary_configs(dev):
     # ---- one empc training step of the IL loop (il_exp.py:297-352):
     # MPC forward (lqr_iter 100, eps 1e-4, bounds +-100, T=35) + im_loss backward into the
     # dynamics parameters, cartpole, 4096 problems from config-2 initial states
+    # at 4096 problems and at the reference's own n_batch = 32 (il_exp.py:44; one
+    # workgroup: the whole stop-rule loop in one launch, dilqr_mpc_solve_small_f32)
     from dilqr import il
+    import warnings
     env = il.IL_Env("cartpole", lqr_iter=100, mpc_T=35, device=dev)
-    Bi = 4096
-    xi = torch.tensor(make_problems(Bi, seed=2)[0], device=dev)
-    params = torch.tensor((9.8, 3.0, 0.1, 1.0), device=dev, requires_grad=True)
     qi, pi_ = env.true_dx.get_true_obj()
     qi, pi_ = qi.to(dev), pi_.to(dev)
-    target = torch.zeros(35, Bi, 1, device=dev)
+    for Bi, key in ((4096, "il_empc_step_cartpole"), (32, "il_empc_step_cartpole_b32")):
+        xi = torch.tensor(make_problems(Bi, seed=2)[0], device=dev)
+        params = torch.tensor((9.8, 3.0, 0.1, 1.0), device=dev, requires_grad=True)
+        target = torch.zeros(35, Bi, 1, device=dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        fwd, bwd = [], []
 
-    def il_step():
-        params.grad = None
-        _, uu = env.mpc(CartpoleDx(params), xi, qi, pi_)
-        loss = (target - uu).pow(2).mean()
-        loss.backward()
-    import warnings
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")
-        il_step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(3):
+        def il_step(rec=False):
+            params.grad = None
+            if rec:
+                ev[0].record()
+            _, uu = env.mpc(CartpoleDx(params), xi, qi, pi_)
+            if rec:
+                ev[1].record()
+            loss = (target - uu).pow(2).mean()
+            loss.backward()
+            if rec:
+                ev[2].record()
+                torch.cuda.synchronize()
+                fwd.append(ev[0].elapsed_time(ev[1]))
+                bwd.append(ev[1].elapsed_time(ev[2]))
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
             il_step()
-        torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / 3
-    out["il_empc_step_cartpole"] = {"ms_per_step": ms, "batch": Bi, "T": 35, "lqr_iter_max": 100,
-                                    "what": "MPC forward to the stop rule + implicit backward into theta"}
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                il_step()
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / 3
+            il_step(rec=True)
+        out[key] = {"ms_per_step": ms, "batch": Bi, "T": 35, "lqr_iter_max": 100,
+                    "forward_ms": fwd[0], "backward_ms": bwd[0],
+                    "forward_path": ("one launch (dilqr_mpc_solve_small_f32)" if Bi <= 256
+                                     else "two launches per iteration, host poll every 8"),
+                    "what": "MPC forward to the stop rule + implicit backward into theta"}
     return out
 
 

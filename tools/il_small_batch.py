@@ -59,5 +59,6 @@ def measure(B, reps=5, dev=torch.device("cuda", 0)):
 if __name__ == "__main__":
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
-        out = [measure(B) for B in (32, 4096)]
+        sizes = [int(a) for a in sys.argv[1:]] or [32, 4096]
+        out = [measure(B) for B in sizes]
     print(json.dumps(out), flush=True)
