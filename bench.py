@@ -442,23 +442,28 @@ def secondary_configs(dev):
     # lane-pair search through HBM (written once, read once)
     cf = iter_cost_floats(sv.cost_sym.cpu().numpy(), T=T, d=d)
     it_bytes = float((iter_bytes_per_problem(cf, T=T, n=n, d=d) + 4 * 2 * T * (m * n + m)).sum())
+    boundary = float(iter_bytes_per_problem(cf, T=T, n=n, d=d).sum())            # 4,028 B/problem
     survey_bytes = 4 * (T * d * d + T * d + n + 2 * T * d + 2) * B             # 36,540 B/problem, SURVEY §8(d)
     gbs = it_bytes / (it_ms * 1e-3) / 1e9
     out["config3_rocket"] = {
         "value": val, "unit": "problem-iters/s", "ms_per_iter": ms_it, "batch": B, "T": T,
         "fused_iteration": with_pmc(
-            {"kernel": "k_mpc_sweep_g8<Rocket,UNC,register cost> + k_mpc_search_lane<Rocket,NONE,register cost> "
-                       "(+ the dense-cost instantiations, which leave at once): one MPC iteration of the timed "
-                       "solves, steady state",
+            {"kernel": "k_mpc_sweep_g8<Rocket,UNC,register cost> + k_mpc_search_quad<Rocket,NONE,register cost> "
+                       "(+ the dense-cost instantiations on a small grid, which leave at once): one MPC iteration of "
+                       "the timed solves, steady state",
              "bound": "hbm", "avg_launch_ms": it_ms, "algorithmic_bytes_per_launch": it_bytes,
              "bytes_model": "cost as read (time-invariant diagonal: 2d floats in registers) + x_init + tau in/out "
                             "+ cost, du_norm + gain records through HBM (2 T (mn+m) floats)",
              "survey_bytes_per_launch": survey_bytes,
              "survey_bytes_note": "SURVEY.md §8(d) 36,540 B/problem counts the caller's C at every step, which the "
                                   "steady kernels never read (not a roofline figure)",
-             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
+             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+             "boundary_bytes_per_launch": boundary,
+             "boundary_bytes_model": "what crosses the iteration's boundary: the register cost (2d), x_init, tau in "
+                                     "and out, cost and du_norm per problem (no gain records)",
+             "frac_on_boundary_bytes": boundary / (it_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             ("k_mpc_sweep_g8<Rocket, 0, true>", "k_mpc_sweep_g8<Rocket, 0, false>",
-             "k_mpc_search_lane<Rocket, 0, true>", "k_mpc_search_lane<Rocket, 0, false>")),
+             "k_mpc_search_quad<Rocket, 0, true>", "k_mpc_search_quad<Rocket, 0, false>")),
         "riccati_sweep": sweep_roofline(n, m, T, B, dev)}
     # rocket implicit backward (16-lane groups) at the solution of the timed solves
     x, u = sv.gather_best()
