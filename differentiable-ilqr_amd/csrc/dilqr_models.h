@@ -47,11 +47,21 @@ struct Pendulum {
     o[2] = newdth;
   }
 
+  // cos and sin of the integrated angle at the UNCLAMPED u, as the Jacobian
+  // uses them (and the implicit backward's second-order terms, which take them
+  // as inputs: gen::PendulumD2 next_cs is the same pair by atan2f/cosf/sinf)
+  DEV void next_cs(const float (&x)[N], const float (&u)[M], float& cs, float& sn) const {
+    angle_step(x[0], x[1], DT * (DT * (kg * x[1] + ku * u[0]) + x[2]), cs, sn);
+  }
+
   // pendulum.py:444-475
   DEV void jacobian(const float (&x)[N], const float (&u)[M], float (&D)[N][N + M]) const {
-    float c = x[0], s = x[1], dth = x[2], uu = u[0];
     float sn, cs;
-    angle_step(c, s, DT * (DT * (kg * s + ku * uu) + dth), cs, sn);
+    next_cs(x, u, cs, sn);
+    jacobian_sc(x, u, cs, sn, D);
+  }
+  DEV void jacobian_sc(const float (&x)[N], const float (&u)[M], float cs, float sn, float (&D)[N][N + M]) const {
+    float c = x[0], s = x[1];
     float ir2 = vrcp(c * c + s * s);
     float dc = -s * ir2;                // d newth / d cos
     float ds = c * ir2 + DT * DT * kg;  // d newth / d sin
@@ -171,10 +181,16 @@ struct Cartpole {
     o[4] = dth + DT * th_acc;
   }
 
+  // cos and sin of the integrated angle (independent of u), as forward() and the
+  // Jacobian form them (gen::CartpoleD2 next_cs: the same pair by atan2f/cosf/sinf)
+  DEV void next_cs(const float (&s_)[N], const float (&)[M], float& cs, float& sn) const {
+    angle_step(s_[2], s_[3], DT * s_[4], cs, sn);
+  }
+
   // cartpole.py:790-839 (closed form of the same derivative)
   DEV void jacobian(const float (&s_)[N], const float (&u)[M], float (&D)[N][N + M]) const {
     float sn, cs;
-    angle_step(s_[2], s_[3], DT * s_[4], cs, sn);
+    next_cs(s_, u, cs, sn);
     jacobian_sc(s_, u, cs, sn, D);
   }
 

@@ -118,8 +118,10 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       float D[n][d];
       float Mt[d][d];
       if (t < T - 1) {
-        md.jacobian(xt, ut, D);
-        D2::lag_hess(theta, xt, ut, lam, Mt);             // lam = lam_{t+1}
+        float cn, sn;                                     // the integrated angle, once per step
+        md.next_cs(xt, ut, cn, sn);
+        md.jacobian_sc(xt, ut, cn, sn, D);
+        D2::lag_hess(theta, xt, ut, lam, cn, sn, Mt);     // lam = lam_{t+1}
       } else {
         zero_D(D);
 #pragma unroll
@@ -236,15 +238,16 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       }
       st2(dC + tb * d * d, dCt);
       st(dc + tb * d, dct);
-      float D[n][d], wx[n], hx[n];
-      md.jacobian(xt, ut, D);             // D_t (t = T-1: only for A_{T-1} of the mu carry)
+      float D[n][d], wx[n], hx[n], cn, sn;
+      md.next_cs(xt, ut, cn, sn);         // the integrated angle, once per step
+      md.jacobian_sc(xt, ut, cn, sn, D);  // D_t (t = T-1: only for A_{T-1} of the mu carry)
       // the carry A_{t+1}^T mu_{t+1} = (D_x,t+1)^T mu_{t+1} + Krev^T (D_u,t+1)^T mu_{t+1},
       // Krev = K[t] of the reversed stack = K_{T-1-t}: the gain grad_input pairs with step t+1
       if (t < T - 1) {
         float Kq[m][n], Mt[d][d], Mp[d][p];
         ld2(Kq, K + ((size_t)(T - 1 - t) * B + b) * m * n);
-        D2::lag_hess(theta, xt, ut, lam, Mt);          // lam = lam_{t+1}
-        D2::lag_dparam(theta, xt, ut, lam, Mp);
+        D2::lag_hess(theta, xt, ut, lam, cn, sn, Mt);  // lam = lam_{t+1}
+        D2::lag_dparam(theta, xt, ut, lam, cn, sn, Mp);
         // w_t = g_t - M_t^T y_t
 #pragma unroll
         for (int k = 0; k < n; ++k) {
@@ -329,7 +332,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
 #pragma unroll
         for (int l = 0; l < n; ++l) mu[l] = hx[l] - dlam[l];
         float ft[n][p];
-        D2::f_theta(theta, xt, ut, ft);
+        D2::f_theta_cs(theta, xt, ut, cn, sn, ft);
 #pragma unroll
         for (int k = 0; k < p; ++k) {
           float s = 0.f;

@@ -24,7 +24,9 @@ extern "C" void MODEL##_lag_hess(const float* th, const float* x, const float* u
   float xx[N], uu[M], ll[N], o[Dd][Dd];                                                      \
   for (int i = 0; i < N; ++i) { xx[i] = x[i]; ll[i] = lam[i]; }                               \
   for (int i = 0; i < M; ++i) uu[i] = u[i];                                                  \
-  dilqr::gen::MODEL##D2::lag_hess(th, xx, uu, ll, o);                                         \
+  float cn, sn;                                                                              \
+  dilqr::gen::MODEL##D2::next_cs(th, xx, uu, cn, sn);                                         \
+  dilqr::gen::MODEL##D2::lag_hess(th, xx, uu, ll, cn, sn, o);                                 \
   for (int i = 0; i < Dd * Dd; ++i) out[i] = (&o[0][0])[i];                                  \
 }                                                                                            \
 extern "C" void MODEL##_lag_dparam(const float* th, const float* x, const float* u,           \
@@ -32,7 +34,9 @@ extern "C" void MODEL##_lag_dparam(const float* th, const float* x, const float*
   float xx[N], uu[M], ll[N], o[Dd][P];                                                       \
   for (int i = 0; i < N; ++i) { xx[i] = x[i]; ll[i] = lam[i]; }                               \
   for (int i = 0; i < M; ++i) uu[i] = u[i];                                                  \
-  dilqr::gen::MODEL##D2::lag_dparam(th, xx, uu, ll, o);                                       \
+  float cn, sn;                                                                              \
+  dilqr::gen::MODEL##D2::next_cs(th, xx, uu, cn, sn);                                         \
+  dilqr::gen::MODEL##D2::lag_dparam(th, xx, uu, ll, cn, sn, o);                               \
   for (int i = 0; i < Dd * P; ++i) out[i] = (&o[0][0])[i];                                   \
 }                                                                                            \
 extern "C" void MODEL##_f_theta(const float* th, const float* x, const float* u, float* out) { \
@@ -40,6 +44,14 @@ extern "C" void MODEL##_f_theta(const float* th, const float* x, const float* u,
   for (int i = 0; i < N; ++i) xx[i] = x[i];                                                  \
   for (int i = 0; i < M; ++i) uu[i] = u[i];                                                  \
   dilqr::gen::MODEL##D2::f_theta(th, xx, uu, o);                                              \
+  for (int i = 0; i < N * P; ++i) out[i] = (&o[0][0])[i];                                    \
+}                                                                                            \
+extern "C" void MODEL##_f_theta_cs(const float* th, const float* x, const float* u, float* out) { \
+  float xx[N], uu[M], o[N][P], cn, sn;                                                       \
+  for (int i = 0; i < N; ++i) xx[i] = x[i];                                                  \
+  for (int i = 0; i < M; ++i) uu[i] = u[i];                                                  \
+  dilqr::gen::MODEL##D2::next_cs(th, xx, uu, cn, sn);                                         \
+  dilqr::gen::MODEL##D2::f_theta_cs(th, xx, uu, cn, sn, o);                                   \
   for (int i = 0; i < N * P; ++i) out[i] = (&o[0][0])[i];                                    \
 }
 WRAP(Pendulum, 4, 3, 1, 3)
@@ -115,6 +127,9 @@ def test_generated_second_order_terms(shim, golden, name, cls):
         Mh = call(shim, f"{name}_lag_hess", th, x32, u32, l32, out_size=d * d).reshape(d, d)
         Mp = call(shim, f"{name}_lag_dparam", th, x32, u32, l32, out_size=d * p).reshape(d, p)
         ft = call(shim, f"{name}_f_theta", th, x32, u32, out_size=n * p).reshape(n, p)
+        # the implicit backward's form: cos/sin of the integrated angle as inputs
+        ft_cs = call(shim, f"{name}_f_theta_cs", th, x32, u32, out_size=n * p).reshape(n, p)
+        assert np.abs(ft_cs - ft).max() / max(1.0, np.abs(ft).max()) < 1e-6, b
         Dtau = np.concatenate([Dx[b], Du[b]], -1)
         ref_Mh = np.einsum("i,ijk->jk", lam, Dtau)
         ref_Mp = np.einsum("i,ijk->jk", lam, Dp[b])

@@ -153,10 +153,36 @@ def model_block(M, cls_name):
     unpack_l = unpack_lines(xs, us, ps, lam)[len(unpack):]
     sig = f"const float* __restrict__ th, const float (&x)[{n}], const float (&u)[{m}]"
 
+    # The angle models' second-order terms hold cos and sin of ONE angle: the
+    # integrated angle atan2(sin, cos) + dt * (...) of the next state.  The
+    # device computes that pair once per step through the model's angle_step
+    # (Model::next_cs, the Jacobian's own cos/sin), so the functions the
+    # implicit backward calls take it as (cn, sn) instead of re-evaluating
+    # atan2f, cosf and sinf in each of them; next_cs here evaluates the symbolic
+    # expression (the host test's reference for the pair).
+    trig = set()
+    for e in [x for row in Mh for x in row] + [x for row in Mp for x in row] + [x for row in ft for x in row]:
+        trig |= {a.args[0] for a in sp.sympify(e).atoms(sp.sin, sp.cos)}
+    assert len(trig) <= 1, trig
+    cn_, sn_ = sp.symbols("cn sn", real=True)
+    if trig:
+        A = trig.pop()
+        sub = lambda e: sp.sympify(e).subs({sp.cos(A): cn_, sp.sin(A): sn_})  # noqa: E731
+    else:
+        A, sub = None, (lambda e: e)
+    sig_cs = ", float cn, float sn"
+
     def fn(name, extra_sig, outs, out_decl, with_lam):
         body = emit(name, sig + extra_sig, outs, out_decl, None)
         head, rest = body.split("{", 1)
         return head + "{\n" + unpack + (unpack_l if with_lam else "") + rest
+
+    if A is not None:
+        nc = emit("next_cs", sig, [("cn", sp.cos(A)), ("sn", sp.sin(A))], "float& cn, float& sn", None)
+        head, rest = nc.split("{", 1)
+        next_cs = head + "{\n" + unpack + rest
+    else:
+        next_cs = ("  static DEV void next_cs(" + sig + ", float& cn, float& sn) { cn = 0.f; sn = 0.f; }")
 
     # get_matrices (cartpole.py:105-716, pendulum.py:152-382): D_grad_params
     # [n][d][p] (with the reference's overrides), D_grad_x [n][d][n], D_grad_u
@@ -180,11 +206,16 @@ def model_block(M, cls_name):
     parts = [f"struct {cls_name} {{",
              f"  static constexpr int N = {n}, M = {m}, P = {p}, D = {d};",
              emit_ptr("matrices", sig + ", " + MAT_SIG, mats, unpack),
-             fn("lag_hess", f", const float (&lam)[{n}]",
-                [(f"Mo[{j}][{k}]", Mh[j][k]) for j in range(d) for k in range(d)], f"float (&Mo)[{d}][{d}]", True),
-             fn("lag_dparam", f", const float (&lam)[{n}]",
-                [(f"Mo[{j}][{k}]", Mp[j][k]) for j in range(d) for k in range(p)], f"float (&Mo)[{d}][{p}]", True),
+             next_cs,
+             fn("lag_hess", f", const float (&lam)[{n}]" + sig_cs,
+                [(f"Mo[{j}][{k}]", sub(Mh[j][k])) for j in range(d) for k in range(d)], f"float (&Mo)[{d}][{d}]",
+                True),
+             fn("lag_dparam", f", const float (&lam)[{n}]" + sig_cs,
+                [(f"Mo[{j}][{k}]", sub(Mp[j][k])) for j in range(d) for k in range(p)], f"float (&Mo)[{d}][{p}]",
+                True),
              fn("f_theta", "", [(f"Fo[{i}][{k}]", ft[i][k]) for i in range(n) for k in range(p)],
+                f"float (&Fo)[{n}][{p}]", False),
+             fn("f_theta_cs", sig_cs, [(f"Fo[{i}][{k}]", sub(ft[i][k])) for i in range(n) for k in range(p)],
                 f"float (&Fo)[{n}][{p}]", False),
              "};"]
     return "\n".join(parts)
