@@ -239,3 +239,69 @@ def test_small_batch_solve_equals_per_iteration_launches(model, B, bounds, eps, 
     for f in ("best_cost", "best_du", "full_du_norm", "cost", "alpha", "slot", "improved"):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
     del keep
+
+
+@pytest.mark.parametrize("mls,decay,bounds", [(1, 0.2, None), (2, 0.5, None), (3, 0.2, None), (4, 0.2, None),
+                                              (6, 0.3, None), (9, 0.2, None), (6, 0.2, (-5.0, 5.0))])
+def test_rocket_quad_search_any_max_ls_equals_unfused(golden, mls, decay, bounds):
+    """The rocket MPC's quad-lane line search (k_mpc_search_quad: four passes per
+    round, cost only, pass 0 written speculatively, the winner re-rolled) over
+    max_ls from 1 (the only pass is the last: accepted unrolled-for-comparison)
+    to 9 (three rounds, the last pass alone in round 2): iterates, costs and
+    best iterates equal the unfused kernels' sequential search bit for bit."""
+    import dilqr
+    from dilqr import ops
+    from dilqr.env_dx.rocket import RocketDx
+    g = golden("mpc_f64")
+    x0 = g["rocket_unc_x0"]
+    T, it = 30, 8
+    dx = RocketDx()
+    B = x0.shape[0]
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV)
+    c = p.repeat(T, B, 1).to(DEV)
+    lo, hi = bounds if bounds else (None, None)
+    xi = torch.tensor(x0, dtype=torch.float32, device=DEV)
+    m = dilqr.MPC(13, 3, T, u_lower=lo, u_upper=hi, lqr_iter=it, eps=0.0, not_improved_lim=10 ** 9,
+                  linesearch_decay=decay, max_linesearch_iter=mls, exit_unconverged=False, detach_unconverged=False)
+    with torch.no_grad():
+        xa, ua, ca = m(xi, dilqr.QuadCost(C, c), dx)
+    ws = ops.mpc_solve_unfused(dx.model_id, ops.theta_of(dx, C), xi, C, c, T, u_lower=lo, u_upper=hi, lqr_iter=it,
+                               eps=0.0, linesearch_decay=decay, max_linesearch_iter=mls, not_improved_lim=10 ** 9)
+    alphas = m.last_solve.alpha.cpu().numpy()
+    print(f"max_ls {mls} decay {decay}: final step sizes {np.unique(alphas)}")
+    for a, b in ((xa, ws.best_x), (ua, ws.best_u), (ca, ws.best_cost)):
+        assert torch.equal(a, b), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("B,T,iters,mls", [(1, 1, 1, 1), (3, 2, 3, 1), (5, 7, 1, 2), (129, 4, 6, 2)])
+def test_small_batch_solve_edges(B, T, iters, mls):
+    """The one-workgroup solve at its edges — one problem, a one-step horizon,
+    one iteration (the rule never applied), one line-search pass, a batch that
+    is not a multiple of 64 — equals begin + the per-iteration launches."""
+    from dilqr import _native as N
+    from dilqr import ops
+    from dilqr.env_dx.cartpole import CartpoleDx
+    dx = CartpoleDx()
+    rng = np.random.RandomState(T * 100 + B)
+    th = rng.uniform(-np.pi, np.pi, B)
+    x0 = torch.tensor(np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                                rng.uniform(-1, 1, B)], 1), dtype=torch.float32, device=DEV)
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV).contiguous()
+    c = p.repeat(T, B, 1).to(DEV).contiguous()
+    th_ = ops.theta_of(dx, x0)
+    nb, keep = N.make_bounds(None, None)
+    a = ops.MPCSolve(T, B, 5, 1, DEV)
+    a.solve_small(dx.model_id, th_, x0, C, c, nb, 0.5, mls, iters, 1e-4, 1e-3, 2)
+    b = ops.MPCSolve(T, B, 5, 1, DEV)
+    b.begin(dx.model_id, th_, x0)
+    for i in range(iters):
+        b.iterate(dx.model_id, th_, x0, C, c, nb, 0.5, mls, i, 1e-4, 1e-3, 2)
+    assert a.iterations == (b.iterations if b.stopped else iters) and a.stopped == b.stopped
+    xa, ua = a.gather_best()
+    xb, ub = b.gather_best()
+    assert torch.equal(xa, xb) and torch.equal(ua, ub)
+    for f in ("best_cost", "best_du", "full_du_norm", "cost", "alpha"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    del keep
