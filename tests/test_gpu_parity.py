@@ -776,6 +776,12 @@ def test_implicit_backward_full_size():
                                        c[:, sl].contiguous(), None, None, x[:, sl].contiguous(),
                                        u[:, sl].contiguous(), K[:, sl].contiguous(), -10.0, 10.0, None)
     assert torch.equal(dth[sl], dth2) and torch.equal(dC[:, sl], dC2)
+    # 130 problems: a partial last wave — the same bits
+    sl4 = slice(1000, 1130)
+    dC4, dc4, dth4 = implicit_backward(dx, wx[:, sl4].contiguous(), wu[:, sl4].contiguous(), C[:, sl4].contiguous(),
+                                       c[:, sl4].contiguous(), None, None, x[:, sl4].contiguous(),
+                                       u[:, sl4].contiguous(), K[:, sl4].contiguous(), -10.0, 10.0, None)
+    assert torch.equal(dth4[:128], dth2) and torch.equal(dC4[:, :128], dC2) and torch.equal(dc4[:, :128], dc2)
     # the same slice with every off-diagonal entry of C written as -0.0: not
     # bitwise a diagonal cost, so the backward re-reads C_t in its last pass
     # instead of taking the diagonal from registers — the same values, so the
@@ -787,6 +793,44 @@ def test_implicit_backward_full_size():
                                        c[:, sl].contiguous(), None, None, x[:, sl].contiguous(),
                                        u[:, sl].contiguous(), K[:, sl].contiguous(), -10.0, 10.0, None)
     assert torch.equal(dth3, dth2) and torch.equal(dC3, dC2) and torch.equal(dc3, dc2)
+
+
+@pytest.mark.parametrize("tag", ["cart_unc", "cart_box", "pend_box"])
+@pytest.mark.parametrize("cost", ["diag", "varying"])
+def test_implicit_backward_batch_independent(golden, tag, cost):
+    """The golden problems tiled to B = 128 (two full waves) and 129 (a partial
+    third wave): the first 128 problems' dC, dc, dtheta bit for bit, and the
+    per-problem dtheta against the reference's at 1e-4.  "varying": C_t and
+    c_t scaled per step, so pass D re-reads the caller's C and c instead of
+    holding them in registers."""
+    from dilqr import ops
+    from dilqr.implicit import implicit_backward
+    g = golden("implicit_f64")
+    mname, bounds = IMPLICIT[tag]
+    dx = dilqr_models()[mname]()
+    x, u, Q, P, F, x0, wx, wu = (gpu(g[f"{tag}_{k}"]) for k in ("x", "u", "Q", "P", "F", "x0", "wx", "wu"))
+    T, B0, n = x.shape
+    m = u.shape[2]
+    lo, hi = bounds if bounds else (None, None)
+    if cost == "varying":
+        s = torch.linspace(0.5, 1.5, T, device=DEV)
+        Q = Q * s[:, None, None, None]
+        P = P * s[:, None, None]
+
+    def tile(a, Bt):
+        reps = [1] * a.dim()
+        reps[1] = (Bt + B0 - 1) // B0
+        return a.repeat(*reps)[:, :Bt].contiguous()
+
+    out = {}
+    for Bt in (128, 129):
+        xt, ut, Qt, Pt, Ft = tile(x, Bt), tile(u, Bt), tile(Q, Bt), tile(P, Bt), tile(F, Bt)
+        K, _, _ = ops.lqr_backward(Qt, Pt, Ft, n, m, x=xt, u=ut, u_lower=lo, u_upper=hi)
+        out[Bt] = implicit_backward(dx, tile(wx, Bt), tile(wu, Bt), Qt, Pt, Ft, None, xt, ut, K, lo, hi, None)
+    (dC, dc, dth), (dC1, dc1, dth1) = out[128], out[129]
+    assert torch.equal(dth, dth1[:128]) and torch.equal(dC, dC1[:, :128]) and torch.equal(dc, dc1[:, :128])
+    if cost == "diag":
+        assert relerr(cpu(dth[:B0]), g[f"{tag}_dtheta_b"]) < 1e-4
 
 
 def rocket_x0(B, seed=0):
