@@ -313,13 +313,30 @@ struct FRows {
 // One step.  U: this lane's column of V_{t+1} (lane n: v_{t+1}), replaced by
 // V_t's.  LAST (t = T-1): V_{t+1} = 0 and F = 0, so Q = C + 0, q = c_back + 0.
 // col: this lane's gain column (lane j < n: K[:, j], lanes >= n: k).
-template <int n, int m, int MODE, class FS, bool LAST, class FA, class LdsT>
-DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const float (&Crow)[n + m], float cb_r,
-                              const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&col)[m],
-                              float (&prev_k)[m], bool& have_prev, int& n_qp) {
+// The cost row reaches the step through `cost(Crow, cb_r)`, called where the
+// row is first needed (after the W^T exchange): a caller that loads it from HBM
+// there keeps it out of the registers live across V^T F (the standalone sweep at
+// 4 waves per SIMD); CostRegs passes a row already in registers.
+template <int d>
+struct CostRegs {
+  const float (&C)[d];
+  float cb;
+  DEV void operator()(float (&o)[d], float& ocb) const {
+#pragma unroll
+    for (int j = 0; j < d; ++j) o[j] = C[j];
+    ocb = cb;
+  }
+};
+
+template <int n, int m, int MODE, class FS, bool LAST, class FA, class LdsT, class CP>
+DEV void group_riccati_step_c(LdsT& L, int r, const FA& F, float (&U)[n], const CP& cost, const float (&zI)[m],
+                              const float (&lb)[m], const float (&ub)[m], float (&col)[m], float (&prev_k)[m],
+                              bool& have_prev, int& n_qp) {
   constexpr int d = n + m;
   float Q[d], qr;
   if constexpr (LAST) {
+    float Crow[d], cb_r;
+    cost(Crow, cb_r);
 #pragma unroll
     for (int j = 0; j < d; ++j) Q[j] = Crow[j] + 0.f;
     qr = cb_r + 0.f;
@@ -341,6 +358,8 @@ DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const 
     float Wc[n + 1];
 #pragma unroll
     for (int l = 0; l <= n; ++l) Wc[l] = L.Wt[l][r];
+    float Crow[d], cb_r;
+    cost(Crow, cb_r);
 #pragma unroll
     for (int i = 0; i < d; ++i) {                  // row r of F^T V F = column r of F^T (V^T F)
       float s = 0.f;
@@ -416,6 +435,14 @@ DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const 
   }
 }
 
+template <int n, int m, int MODE, class FS, bool LAST, class FA, class LdsT>
+DEV void group_riccati_step_t(LdsT& L, int r, const FA& F, float (&U)[n], const float (&Crow)[n + m], float cb_r,
+                              const float (&zI)[m], const float (&lb)[m], const float (&ub)[m], float (&col)[m],
+                              float (&prev_k)[m], bool& have_prev, int& n_qp) {
+  group_riccati_step_c<n, m, MODE, FS, LAST>(L, r, F, U, CostRegs<n + m>{Crow, cb_r}, zI, lb, ub, col, prev_k,
+                                             have_prev, n_qp);
+}
+
 // standalone sweep, F from HBM (the LinDx / classic path and the north-star
 // kernel for rocket shapes): F's rows through LDS, dense
 template <int n, int m, int MODE>
@@ -445,14 +472,8 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
   auto step = [&](int t, auto last_c) {
     constexpr bool LAST = decltype(last_c)::value;
     const size_t tb = (size_t)t * B + bb;
-    float Crow[d], cb = 0.f, tau_r = 0.f;
-#pragma unroll
-    for (int j = 0; j < d; ++j) Crow[j] = 0.f;
-    if (r < d) {
-      ld(Crow, C + (tb * d + r) * d);
-      cb = c[tb * d + r];
-      if (x) tau_r = r < n ? x[tb * n + r] : u[tb * m + (r - n)];
-    }
+    float tau_r = 0.f;
+    if (r < d && x) tau_r = r < n ? x[tb * n + r] : u[tb * m + (r - n)];
     if constexpr (!LAST) {
       if (r < n) {
         float Fr[d];
@@ -463,12 +484,22 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
     }
     if (r < d) L.tau[r] = tau_r;
     __syncthreads();
-    if (x && r < d) {
-      float s = 0.f;
+    // the cost row and c_back = c + C tau, loaded where the step first needs them
+    auto cost = [&](float (&Crow)[d], float& cb) {
 #pragma unroll
-      for (int j = 0; j < d; ++j) s += Crow[j] * L.tau[j];
-      cb = s + cb;
-    }
+      for (int j = 0; j < d; ++j) Crow[j] = 0.f;
+      cb = 0.f;
+      if (r < d) {
+        ld(Crow, C + (tb * d + r) * d);
+        cb = c[tb * d + r];
+        if (x) {
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < d; ++j) s += Crow[j] * L.tau[j];
+          cb = s + cb;
+        }
+      }
+    };
     float zIt[m], lb[m], ub[m], ut[m];
 #pragma unroll
     for (int a = 0; a < m; ++a) {
@@ -482,7 +513,7 @@ __global__ void __launch_bounds__(64) k_lqr_backward_group(int T, int B, const f
     }
     float col[m];
     const int qp_before = nqp;
-    group_riccati_step_t<n, m, MODE, DenseF, LAST>(L, r, FRows<n, m>{L}, U, Crow, cb, zIt, lb, ub, col, prev_k,
+    group_riccati_step_c<n, m, MODE, DenseF, LAST>(L, r, FRows<n, m>{L}, U, cost, zIt, lb, ub, col, prev_k,
                                                    have_prev, nqp);
     if (MODE == GAIN_BOX && valid && n_qp_step && r == 0) atomicMax(n_qp_step + t, nqp - qp_before - 1);
     if (valid) {
