@@ -542,6 +542,45 @@ def test_full_size_batch_independence():
     assert torch.isfinite(full[2]).all()
 
 
+@pytest.mark.parametrize("bounds", [None, (-10.0, 10.0)])
+def test_max_batch_one_gpu(bounds):
+    """Config 5's whole batch (B = 524 288, 8x a GPU's shard) on one GPU, the
+    solve and the implicit backward: the last 256 problems (the highest record
+    offsets, where a 32-bit index would wrap first) solved alone give the same
+    iterates and gradients bit for bit."""
+    from dilqr import ops
+    from dilqr.implicit import implicit_backward
+    B, T, S = 524288, 25, 256
+    rng = np.random.RandomState(3)
+    th = rng.uniform(-np.pi, np.pi, B)
+    x0 = np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                   rng.uniform(-1, 1, B)], 1)
+    full = run_gpu_mpc(x0, "cartpole", T, 3, bounds, 0.0, 10 ** 9, 0.5, 2)
+    part = run_gpu_mpc(x0[B - S:], "cartpole", T, 3, bounds, 0.0, 10 ** 9, 0.5, 2)
+    assert torch.equal(full[1][:, B - S:], part[1]) and torch.equal(full[2][B - S:], part[2])
+    assert torch.isfinite(full[2]).all()
+    dx = dilqr_models()["cartpole"]()
+    q, p = dx.get_true_obj()
+    lo, hi = bounds if bounds else (None, None)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    wx = torch.randn(T, B, 5, device=DEV, generator=g)
+    wu = torch.randn(T, B, 1, device=DEV, generator=g)
+    out = []
+    for sl in (slice(0, B), slice(B - S, B)):
+        Bs = sl.stop - sl.start
+        C = torch.diag(q).repeat(T, Bs, 1, 1).to(DEV)
+        c = p.repeat(T, Bs, 1).to(DEV)
+        x, u = full[0][:, sl].contiguous(), full[1][:, sl].contiguous()
+        F = ops.linearize(dx.model_id, ops.theta_of(dx, C), x, u)[0]
+        K, _, _ = ops.lqr_backward(C, c, F, 5, 1, x=x, u=u, u_lower=lo, u_upper=hi)
+        out.append(implicit_backward(dx, wx[:, sl].contiguous(), wu[:, sl].contiguous(), C, c, None, None, x, u, K,
+                                     lo, hi, None))
+        del C, c, F
+    (dC, dc, dth), (dC2, dc2, dth2) = out
+    assert torch.equal(dth[B - S:], dth2) and torch.equal(dC[:, B - S:], dC2) and torch.equal(dc[:, B - S:], dc2)
+    assert torch.isfinite(dth).all()
+
+
 @pytest.mark.parametrize("name", ["cart_unc", "cart_box10", "pend_box", "rocket_unc"])
 def test_fixed_count_solve_equals_stop_rule_path(golden, name):
     """A solve whose stop rule cannot fire (eps <= 0, not_improved_lim >= the
@@ -1014,12 +1053,14 @@ def test_rocket_fused_iteration_equals_unfused_tensor_bounds(golden):
     assert at_bound > 0.0 and (np.abs(u) <= half.numpy() + 1e-6).all()
 
 
-def test_rocket_mpc_full_size_batch_independence():
-    """Config 3 shape (B=32768, T=30): a solve over the whole batch returns, for
-    a sample of problems, what solving those problems alone returns."""
+@pytest.mark.parametrize("B", [32768, 131072])
+def test_rocket_mpc_full_size_batch_independence(B):
+    """Config 3 shape (B=32768, T=30) and 4x that batch on one GPU: a solve
+    over the whole batch returns, for a sample of problems (the last one
+    included), what solving those problems alone returns."""
     import dilqr
     from dilqr.env_dx.rocket import RocketDx
-    T, B = 30, 32768
+    T = 30
     rng = np.random.RandomState(3)
     x0 = np.concatenate([rng.uniform([0, -4, -2.5], [10, 4, 2.5], (B, 3)), rng.normal(0, 0.1, (B, 3)),
                          np.tile([1., 0, 0, 0], (B, 1)) + 0.05 * rng.normal(size=(B, 4)),
@@ -1038,7 +1079,7 @@ def test_rocket_mpc_full_size_batch_independence():
 
     x, u, cost = solve(x0)
     assert torch.isfinite(cost).all()
-    idx = np.array([0, 1, 4097, 12345, B - 1])
+    idx = np.array([0, 1, 4097, 12345, B - 2, B - 1])
     xs, us, cs = solve(x0[idx])
     print(f"rocket batch independence: max |du| {float((u[:, idx] - us).abs().max()):.3e}, "
           f"max |dcost| {float((cost[idx] - cs).abs().max()):.3e}")
