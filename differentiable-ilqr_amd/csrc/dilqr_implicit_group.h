@@ -19,6 +19,13 @@
 
 #include "dilqr_group.h"
 
+#ifndef DILQR_IMPL_SKIP
+#define DILQR_IMPL_SKIP 0
+#endif
+#ifndef DILQR_IMPL_C_PF
+#define DILQR_IMPL_C_PF 1
+#endif
+
 namespace dilqr {
 
 // per-(t,b) workspace record (floats), written lane-contiguous: what pass C
@@ -184,17 +191,36 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
   // per lane: row r of C and c_t[r] from registers in pass D
   const bool crow_regs = c_offd == 0u && c_dif == 0u, cv_regs = cv_dif == 0u;
   // ---------------- C (t up): the rollout y of the modified problem (linear, alpha = 1)
+  // (DILQR_IMPL_SKIP: timing-only builds that leave out pass C (bit 1) or pass D
+  // (bit 2) to split the kernel's time by pass; never the shipped library)
   {
     float yx = 0.f;                                        // lane r < n: y_t[r]
-    for (int t = 0; t < T; ++t) {
-      const size_t tb = (size_t)t * B + b;
-      float* R0 = rec(t);
-      float xt[n], ut[m], Kc[m], kt[m];
-      load_tau(tb, xt, ut);
+    // DILQR_IMPL_C_PF: step t+1's inputs (x, u, this lane's gain column, k)
+    // loaded while step t computes — pass C is a short chain per step behind its
+    // loads, and its live set is far below the kernel's peak (passes B and D)
+    float xq[n], uq[m], Kq_[m], kq[m];
+    auto load_c = [&](int t, float (&xs)[n], float (&us)[m], float (&Kc)[m], float (&kt)[m]) {
+      load_tau((size_t)t * B + b, xs, us);
+      const float* R0 = rec(t);
 #pragma unroll
       for (int a = 0; a < m; ++a) {
         Kc[a] = r < n ? R0[W::KG + a * kG + r] : 0.f;
         kt[a] = R0[W::KG + a * kG + n];
+      }
+    };
+    if (DILQR_IMPL_C_PF && T > 0) load_c(0, xq, uq, Kq_, kq);
+    for (int t = 0; t < ((DILQR_IMPL_SKIP & 1) ? 0 : T); ++t) {
+      const size_t tb = (size_t)t * B + b;
+      float* R0 = rec(t);
+      float xt[n], ut[m], Kc[m], kt[m];
+      if (DILQR_IMPL_C_PF) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) xt[i] = xq[i];
+#pragma unroll
+        for (int a = 0; a < m; ++a) { ut[a] = uq[a]; Kc[a] = Kq_[a]; kt[a] = kq[a]; }
+        if (t + 1 < T) load_c(t + 1, xq, uq, Kq_, kq);
+      } else {
+        load_c(t, xt, ut, Kc, kt);
       }
       // y_t from y_t's state part (the previous step's D y)
       float yr = r < n ? yx : 0.f;
@@ -230,7 +256,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
     for (int a = 0; a < m; ++a) au[a] = 0.f;
     if (r < kG) { I.dlam[r] = 0.f; I.lam[r] = 0.f; }
     __syncthreads();
-    for (int t = T - 1; t >= 0; --t) {
+    for (int t = (DILQR_IMPL_SKIP & 2) ? -1 : T - 1; t >= 0; --t) {
       const size_t tb = (size_t)t * B + b;
       const float* R0 = rec(t);
       float xt[n], ut[m], y[d], Crow[d], cr = 0.f, gr = 0.f;
