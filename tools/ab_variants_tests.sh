@@ -9,7 +9,7 @@ L=differentiable-ilqr_amd/dilqr/libdilqr.so
 cp $L ab/.inplace.so
 K=${AB_TEST_K:-"fused_iteration_equals_unfused or whole_solve or fixed_count or packed_cost or small_batch or mpc_solve_vs_oracle"}
 rc=0
-for f in ab/libdilqr_*.so; do
+for f in ab/${AB_GLOB:-libdilqr_*.so}; do
   v=${f#ab/libdilqr_}; v=${v%.so}
   cp $f $L
   timeout -k 10 300 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "$K" \

@@ -14,12 +14,15 @@ OBJS=()
 for o in $P/build/tu_*.o; do
   tu=$(basename $o .o)
   if [[ " $* " == *" $tu "* ]]; then
+    # the unit's own flags from the Makefile (TUFLAGS_<unit> := ...), as the
+    # in-tree build compiles it, then the variant's
+    TUF=$(sed -n "s/^TUFLAGS_$tu := //p" $P/Makefile)
     /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result -ffp-contract=on \
-        $FLAGS -c -o /tmp/abv/$NAME/$tu.o $P/csrc/$tu.hip
+        $TUF $FLAGS -c -o /tmp/abv/$NAME/$tu.o $P/csrc/$tu.hip
     OBJS+=(/tmp/abv/$NAME/$tu.o)
   else
     OBJS+=($o)
   fi
 done
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -o $R/ab/libdilqr_$NAME.so "${OBJS[@]}"
-echo "built ab/libdilqr_$NAME.so ($FLAGS: $*)"
+echo "built ab/libdilqr_$NAME.so ($FLAGS: $*; unit flags from the Makefile)"
