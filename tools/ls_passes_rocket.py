@@ -1,5 +1,7 @@
-"""Config 3 (rocket): per iteration, the share of problems and of waves (4
-problems) that need more than one paired line-search pass (alpha < decay)."""
+"""Config 3 (rocket): per iteration, the share of problems and of waves that
+need more than one line-search pass (alpha < decay), and how often a problem's
+accepted pass repeats the previous iteration's (a speculative write by the
+previous winner's lane)."""
 import os
 import sys
 
@@ -30,9 +32,10 @@ theta = ops.theta_of(dx, x0)
 sv = ops.MPCSolve(T, B, n, m, dev)
 nb, _ = N.make_bounds(None, None)
 sv.begin(N.MODEL_ROCKET, theta, x0)
+prev = None
 for i in range(10):
     sv.iterate(N.MODEL_ROCKET, theta, x0, C, c, nb, 0.2, 5, i, 1e-4, 0.0, 10 ** 9)
-    al = sv.alpha
+    al = sv.alpha.clone()
     hist = {f"{x:g}": int((al == x).sum()) for x in (1.0, 0.2, 0.04, 0.008, 0.0016)}
     # lane-pair search (today): 32 problems per wave, rounds of 2 candidates
     w32 = al.view(-1, 32)
@@ -44,5 +47,15 @@ for i in range(10):
     # the quad search (k_mpc_search_quad): a wave rewrites (phase 2) when any
     # of its 16 problems accepted a pass other than 0
     ph2 = float((w16 < 1.0).any(1).float().mean())
+    # a speculative write by the lane of each problem's previous winner: the
+    # problems whose winner repeats, and the waves that would still rewrite
+    if prev is not None:
+        same = (al == prev)
+        keep = float(same.float().mean())
+        ph2p = float((~same).view(-1, 16).any(1).float().mean())
+    else:
+        keep, ph2p = float("nan"), float("nan")
+    prev = al
     print(f"iter {i}: alpha hist {hist}; 32-problem waves needing round 2 {r2:.3f}, round 3 {r3:.3f}; "
-          f"16-problem waves needing a 5th candidate {q2:.3f}, a phase-2 rewrite {ph2:.3f}", flush=True)
+          f"16-problem waves needing a 5th candidate {q2:.3f}, a phase-2 rewrite {ph2:.3f}; "
+          f"winner repeats {keep:.4f}, rewrite with previous-winner speculation {ph2p:.3f}", flush=True)
