@@ -872,6 +872,64 @@ def test_implicit_backward_batch_independent(golden, tag, cost):
         assert relerr(cpu(dth[:B0]), g[f"{tag}_dtheta_b"]) < 1e-4
 
 
+@pytest.mark.parametrize("model", ["cartpole", "rocket"])
+@pytest.mark.parametrize("T", [1, 2, 3])
+def test_implicit_backward_short_horizons(model, T):
+    """The implicit backward at horizons of 1-3 steps (at T = 1 the passes
+    degenerate: no dynamics step, the costate recursion and gradx carry never
+    run, dtheta = 0), both kernels (one lane per problem; rocket's 16-lane
+    groups), against the fp64 oracle's fast algebra on the same fp32 solution
+    (1e-4 of the max magnitude; T = 1, which the reference's grad_input cannot
+    form, against the one-step problem's closed form), with bounds active for
+    cartpole."""
+    from dilqr import ops
+    from dilqr.implicit import implicit_backward
+    B = 64
+    if model == "cartpole":
+        rng = np.random.RandomState(T)
+        th = rng.uniform(-np.pi, np.pi, B)
+        x0 = np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                       rng.uniform(-1, 1, B)], 1)
+        bounds, decay, mls, om = (-2.0, 2.0), 0.5, 2, omodels.Cartpole
+    else:
+        x0 = rocket_x0(B, seed=T)
+        bounds, decay, mls, om = None, 0.2, 5, omodels.Rocket
+    x, u, _ = run_gpu_mpc(x0, model, T, 5, bounds, 0.0, 10 ** 9, decay, mls)
+    dx = dilqr_models()[model]()
+    n, m = x.shape[2], u.shape[2]
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV)
+    c = p.repeat(T, B, 1).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(T)
+    wx = torch.randn(T, B, n, device=DEV, generator=g)
+    wu = torch.randn(T, B, m, device=DEV, generator=g)
+    lo, hi = bounds if bounds else (None, None)
+    F = ops.linearize(dx.model_id, ops.theta_of(dx, C), x, u)[0] if T > 1 else None
+    K, _, _ = ops.lqr_backward(C, c, F, n, m, x=x, u=u, u_lower=lo, u_upper=hi)
+    dC, dc, dth = implicit_backward(dx, wx, wu, C, c, None, None, x, u, K, lo, hi, None)
+    so = slice(0, 8)
+    f64 = lambda a: cpu(a[:, so]).astype(np.float64)  # noqa: E731
+    if T == 1:
+        # the reference's grad_input stacks T-1 = 0 dynamics steps and raises,
+        # as the oracle that mirrors it does; the one-step problem's closed
+        # form: y_x = 0, y_u = C_uu^-1 g_u on the free controls (diagonal C
+        # here), 0 on the active ones; dc = -y, dC = -(y tau^T + tau y^T)/2
+        Cn, uu, gu = f64(C)[0], f64(u)[0], f64(wu)[0]
+        act = np.zeros_like(uu, dtype=bool) if lo is None else (np.abs(uu - lo) <= 1e-8) | (np.abs(uu - hi) <= 1e-8)
+        yu = np.where(act, 0.0, gu / np.diagonal(Cn, axis1=1, axis2=2)[:, n:])
+        y = np.concatenate([np.zeros((8, n)), yu], 1)
+        tau = np.concatenate([f64(x)[0], uu], 1)
+        rdc = -y[None]
+        rdC = (-0.5 * (y[:, :, None] * tau[:, None, :] + tau[:, :, None] * y[:, None, :]))[None]
+        assert relerr(cpu(dC[:, so]), rdC) < 1e-5 and relerr(cpu(dc[:, so]), rdc) < 1e-5
+        assert float(dth.abs().max()) == 0.0
+        return
+    rdC, rdc, rdth = oadj.implicit_backward_fast(om, f64(wx), f64(wu), f64(C), f64(c), f64(F), None, f64(x),
+                                                 f64(u), f64(K)[::-1].copy(), lo, hi)
+    assert relerr(cpu(dC[:, so]), rdC) < 1e-4 and relerr(cpu(dc[:, so]), rdc) < 1e-4
+    assert relerr(cpu(dth[so]), rdth) < 1e-4
+
+
 def rocket_x0(B, seed=0):
     """near-hover initial states, SURVEY.md §8(d) config 3"""
     rng = np.random.RandomState(seed)
