@@ -315,8 +315,9 @@ struct FRows {
 // col: this lane's gain column (lane j < n: K[:, j], lanes >= n: k).
 // The cost row reaches the step through `cost(Crow, cb_r)`, called where the
 // row is first needed (after the W^T exchange): a caller that loads it from HBM
-// there keeps it out of the registers live across V^T F (the standalone sweep at
-// 4 waves per SIMD); CostRegs passes a row already in registers.
+// there keeps it out of the registers live across V^T F and its load off the
+// step's top (the standalone sweep: 0.476 -> 0.469 ms at config 3);
+// CostRegs passes a row already in registers.
 template <int d>
 struct CostRegs {
   const float (&C)[d];

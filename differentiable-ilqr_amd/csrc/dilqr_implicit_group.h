@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
     // DILQR_IMPL_C_PF: step t+1's inputs (x, u, this lane's gain column, k)
     // loaded while step t computes — pass C is a short chain per step behind its
     // loads, and its live set is far below the kernel's peak (passes B and D)
-    float xq[n], uq[m], Kq_[m], kq[m];
+    float xq[n], uq[m], Kcq[m], kq[m];
     auto load_c = [&](int t, float (&xs)[n], float (&us)[m], float (&Kc)[m], float (&kt)[m]) {
       load_tau((size_t)t * B + b, xs, us);
       const float* R0 = rec(t);
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         kt[a] = R0[W::KG + a * kG + n];
       }
     };
-    if (DILQR_IMPL_C_PF && T > 0) load_c(0, xq, uq, Kq_, kq);
+    if (DILQR_IMPL_C_PF) load_c(0, xq, uq, Kcq, kq);
     for (int t = 0; t < ((DILQR_IMPL_SKIP & 1) ? 0 : T); ++t) {
       const size_t tb = (size_t)t * B + b;
       float* R0 = rec(t);
@@ -217,8 +217,8 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
 #pragma unroll
         for (int i = 0; i < n; ++i) xt[i] = xq[i];
 #pragma unroll
-        for (int a = 0; a < m; ++a) { ut[a] = uq[a]; Kc[a] = Kq_[a]; kt[a] = kq[a]; }
-        if (t + 1 < T) load_c(t + 1, xq, uq, Kq_, kq);
+        for (int a = 0; a < m; ++a) { ut[a] = uq[a]; Kc[a] = Kcq[a]; kt[a] = kq[a]; }
+        if (t + 1 < T) load_c(t + 1, xq, uq, Kcq, kq);
       } else {
         load_c(t, xt, ut, Kc, kt);
       }
