@@ -297,6 +297,10 @@ constexpr int kPF = DILQR_PF;
 constexpr int kPFL = DILQR_PF_LS;                   // the line search's prefetch distance
 static_assert(kPFL == 1, "the line search prefetches one step ahead");
 
+#ifndef DILQR_PHASE_SKIP
+#define DILQR_PHASE_SKIP 0
+#endif
+
 // ---------------- forward: the line search (lqr_step_explicit.py:166-263).
 // Pass p uses alpha_p = decay^p and is accepted when its cost <= old cost or
 // it is the last pass.  Passes 2r and 2r+1 roll out TOGETHER (candidates A
@@ -611,6 +615,14 @@ DEV int ilqr_problem(int T, int B, int b, const Model md, const float* __restric
     }
   }
   DILQR_STAMP(2);
+#if DILQR_PHASE_SKIP & 1
+  // timing-only builds (tools/small_phase_split.py; never the shipped library):
+  // the iteration ends after the sweep, the trajectory kept, so every iteration
+  // repeats the same sweep and the line search's share is the difference
+  cost_out = old_cost;
+  alpha_out = 1.f;
+  return 0;
+#endif
   if constexpr (!CostT::kDiag && packed_diag_ok<d>()) {
     if (pack_out && sym && diag && tinv) {              // iteration 0 of a diag(q), p over t cost
       CostDiagConst<d> cc;
