@@ -308,12 +308,12 @@ def case_lqrstep():
 # --------------------------------------------------------------------------
 MPC_CASES = {
     # name: (model, T, B, lqr_iter, bounds, eps, not_improved_lim, decay, max_ls)
-    "cart_unc": ("cartpole", 25, 16, 10, None, 0.0, 10 ** 9, 0.5, 2),
-    "cart_box10": ("cartpole", 25, 16, 10, (-10.0, 10.0), 0.0, 10 ** 9, 0.5, 2),
-    "cart_il": ("cartpole", 25, 16, 40, (-100.0, 100.0), 1e-4, 5, 0.5, 2),
-    "pend_unc": ("pendulum", 10, 16, 10, None, 0.0, 10 ** 9, 0.2, 5),
-    "pend_box": ("pendulum", 10, 16, 10, (-2.0, 2.0), 0.0, 10 ** 9, 0.2, 5),
-    "rocket_unc": ("rocket", 30, 4, 5, None, 0.0, 10 ** 9, 0.2, 5),
+    "cart_unc": ("cartpole", 25, 64, 10, None, 0.0, 10 ** 9, 0.5, 2),
+    "cart_box10": ("cartpole", 25, 64, 10, (-10.0, 10.0), 0.0, 10 ** 9, 0.5, 2),
+    "cart_il": ("cartpole", 25, 64, 40, (-100.0, 100.0), 1e-4, 5, 0.5, 2),
+    "pend_unc": ("pendulum", 10, 64, 10, None, 0.0, 10 ** 9, 0.2, 5),
+    "pend_box": ("pendulum", 10, 64, 10, (-2.0, 2.0), 0.0, 10 ** 9, 0.2, 5),
+    "rocket_unc": ("rocket", 30, 64, 5, None, 0.0, 10 ** 9, 0.2, 5),
 }
 
 
@@ -401,14 +401,30 @@ def implicit_once(mname, T, B, bounds, x, u, x0, Q, P, wx, wu, dt):
     return np_(Qg.grad), np_(Pg.grad), np_(theta.grad), np_(F), np_(f)
 
 
-def case_implicit():
-    print("G. implicit backward")
-    cases = {"cart_unc": ("cartpole", 10, 4, None, "cart_unc"),
-             "cart_box": ("cartpole", 10, 4, (-5.0, 5.0), "cart_box10"),
-             "pend_box": ("pendulum", 10, 4, (-2.0, 2.0), "pend_box"),
-             # rocket: the reference's D_x/D_u/D_params/x_xtm1 builders (rocket.py:541-820)
-             "rock_unc": ("rocket", 10, 4, None, "rocket_unc"),
-             "rock_box": ("rocket", 10, 4, (-10.0, 10.0), "rocket_unc")}
+IMPLICIT_CASES = {
+    # tag: (model, T, B, bounds, MPC_CASES entry for decay / max_ls)
+    "cart_unc": ("cartpole", 10, 4, None, "cart_unc"),
+    "cart_box": ("cartpole", 10, 4, (-5.0, 5.0), "cart_box10"),
+    "pend_box": ("pendulum", 10, 4, (-2.0, 2.0), "pend_box"),
+    # rocket: the reference's D_x/D_u/D_params/x_xtm1 builders (rocket.py:541-820)
+    "rock_unc": ("rocket", 10, 4, None, "rocket_unc"),
+    "rock_box": ("rocket", 10, 4, (-10.0, 10.0), "rocket_unc"),
+}
+# config 4's own horizon (SURVEY.md §8(c) case G): cartpole T=25, B=8; T*B=200
+# stays under the reference's CPU-path threshold (lqr_step_explicit.py:699-700)
+IMPLICIT25_CASES = {
+    "cart25_unc": ("cartpole", 25, 8, None, "cart_unc"),
+    "cart25_box10": ("cartpole", 25, 8, (-10.0, 10.0), "cart_box10"),
+    "cart25_box100": ("cartpole", 25, 8, (-100.0, 100.0), "cart_box10"),
+}
+
+
+def case_implicit25():
+    case_implicit(IMPLICIT25_CASES, "implicit25")
+
+
+def case_implicit(cases=IMPLICIT_CASES, fname="implicit"):
+    print(f"G. implicit backward ({fname})")
     for dt in (torch.float64, torch.float32):
         with default_dtype(dt):
             out = {}
@@ -430,7 +446,7 @@ def case_implicit():
                 wu = rng.normal(size=u.shape)
                 # MKL's batched getrf hangs on the rocket's 160x160 KKT systems with
                 # 8 threads in this image (lqr_step_explicit.py:570); one thread is fine
-                torch.set_num_threads(1 if mname == "rocket" else 8)
+                torch.set_num_threads(1 if mname == "rocket" or T * (dx.n_state + dx.n_ctrl) > 100 else 8)
                 dQ, dP, dth, F, f = implicit_once(mname, T, B, bounds, x, u, x0, Q, P, wx, wu, dt)
                 # per-problem d theta: weight only problem j
                 dth_b = []
@@ -442,7 +458,7 @@ def case_implicit():
                             f"{tag}_P": np_(P), f"{tag}_wx": wx, f"{tag}_wu": wu, f"{tag}_F": F,
                             f"{tag}_f": f, f"{tag}_dQ": dQ, f"{tag}_dP": dP, f"{tag}_dtheta": dth,
                             f"{tag}_dtheta_b": np.stack(dth_b)})
-            save(f"implicit_{tname(dt)}", **out)
+            save(f"{fname}_{tname(dt)}", **out)
 
 
 # --------------------------------------------------------------------------
@@ -841,10 +857,10 @@ def case_complex():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["models", "riccati", "pnqp", "lqrstep", "mpc", "adjoint", "implicit",
-                             "datasets", "il", "generic", "api", "complex", "stepgen"]
+                             "implicit25", "datasets", "il", "generic", "api", "complex", "stepgen"]
     table = {"models": case_models, "riccati": case_riccati, "pnqp": case_pnqp,
              "lqrstep": case_lqrstep, "mpc": case_mpc, "adjoint": case_classic_adjoint,
-             "implicit": case_implicit, "datasets": case_datasets, "il": case_il,
+             "implicit": case_implicit, "implicit25": case_implicit25, "datasets": case_datasets, "il": case_il,
              "generic": case_generic, "api": case_api, "complex": case_complex, "stepgen": case_stepgen}
     for w in which:
         table[w]()

@@ -262,7 +262,7 @@ def gpu_solve_with_decisions(x0, mname, T, it, bounds, eps, nil, decay, mls):
 
 
 def check_against_forced_oracle(M, x0, T, bounds, decay, mls, x, u, costs, alphas, takes, label,
-                                cost_tol=1e-5, traj_tol=1e-4, tie=1e-5):
+                                cost_tol=1e-5, traj_tol=1e-4, tie=1e-5, ref_spread=None):
     """Parity by decision replay.  (1) The fp64 oracle, made to take the GPU's
     decisions (its step sizes and best-iterate updates, oracle/mpc.py `force`),
     must reproduce the GPU's best trajectories and costs: what remains is fp32
@@ -271,7 +271,10 @@ def check_against_forced_oracle(M, x0, T, bounds, decay, mls, x, u, costs, alpha
     must equal the GPU's unless the decision is a near-tie (its margin below
     `tie`: |cost_p - old| / |old| for a step size, |cost - (best + eps)| / |best|
     for the best-iterate test), where fp32 and fp64 may legitimately differ.
-    Prints the measured errors and the count of near-tie flips."""
+    Prints the measured errors and the count of near-tie flips.
+    ref_spread (per problem, optional): the reference's own fp32-vs-fp64 cost
+    difference on the same problem; a problem whose cost the reference itself
+    cannot hold to cost_tol in fp32 is held to 3x that spread instead."""
     B = x0.shape[0]
     q, p = M.true_obj()
     Co, co = ompc.expand_cost(np.diag(q), p, T, B)
@@ -294,7 +297,12 @@ def check_against_forced_oracle(M, x0, T, bounds, decay, mls, x, u, costs, alpha
         assert np.all(tr["best_margin"][dif_t] < tie), (label, i, np.flatnonzero(dif_t), tr["best_margin"][dif_t])
     print(f"\n[{label}] forced-decision oracle: max rel cost err {cerr.max():.2e}, u {uerr:.2e}, x {xerr:.2e}; "
           f"near-tie decision flips {flips}/{total}")
-    assert cerr.max() < cost_tol, cerr.max()
+    tol = np.full(B, cost_tol) if ref_spread is None else np.maximum(cost_tol, 3 * ref_spread)
+    wide = np.flatnonzero(tol > cost_tol)
+    if wide.size:
+        print(f"[{label}] problems {wide} held to 3x the reference's own fp32 spread "
+              f"{ref_spread[wide]}: errors {cerr[wide]}")
+    assert np.all(cerr < tol), (np.flatnonzero(cerr >= tol), cerr.max())
     assert uerr < traj_tol and xerr < traj_tol, (uerr, xerr)
     return cso
 
@@ -313,11 +321,16 @@ def test_mpc_solve_vs_oracle(golden, name):
     # the same solve through the public API is the same computation
     x2, u2, costs2 = run_gpu_mpc(x0, mname, T, it, bounds, eps, nil, decay, mls)
     assert same_bits(x, x2) and same_bits(u, u2) and same_bits(costs, costs2)
-    check_against_forced_oracle(omodels.MODELS[mname], x0, T, bounds, decay, mls, x, u, costs, alphas, takes, name)
     ref = g[f"{name}_costs"]
+    # the reference's own fp32 solve of the same problems (B=64): its distance
+    # from the fp64 solve measures each problem's fp32 conditioning (cart_box10
+    # problem 32: 1.45e-4; every other problem of every case: <= 4.3e-6)
+    spread = np.abs(golden("mpc_f32")[f"{name}_costs"] - ref) / np.maximum(1.0, np.abs(ref))
+    check_against_forced_oracle(omodels.MODELS[mname], x0, T, bounds, decay, mls, x, u, costs, alphas, takes, name,
+                                ref_spread=spread)
     rerr = np.abs(cpu(costs) - ref) / np.maximum(1.0, np.abs(ref))
     print(f"[{name}] vs the reference's fp64 costs: max rel {rerr.max():.2e}, median {np.median(rerr):.2e}")
-    assert np.max(rerr) < 1e-4, np.max(rerr)
+    assert np.all(rerr < np.maximum(1e-4, 3 * spread)), (np.flatnonzero(rerr >= 1e-4), rerr.max())
 
 
 COMPLEX_MPC = {"fixed": (20, 10, 0.0, 10 ** 9), "il": (20, 40, 1e-3, 5)}     # T, lqr_iter, eps, not_improved_lim
@@ -729,17 +742,34 @@ def test_whole_solve_launch_equals_per_iteration_launches(golden, name, warm):
 # ------------------------------------------------------------------ DiLQR implicit backward
 IMPLICIT = {"cart_unc": ("cartpole", None), "cart_box": ("cartpole", (-5.0, 5.0)),
             "pend_box": ("pendulum", (-2.0, 2.0)), "rock_unc": ("rocket", None),
-            "rock_box": ("rocket", (-10.0, 10.0))}
+            "rock_box": ("rocket", (-10.0, 10.0)),
+            # config 4's own horizon, cartpole T=25, B=8 (gen_golden.py IMPLICIT25_CASES)
+            "cart25_unc": ("cartpole", None), "cart25_box10": ("cartpole", (-10.0, 10.0)),
+            "cart25_box100": ("cartpole", (-100.0, 100.0))}
 
 
-@pytest.mark.parametrize("tag", list(IMPLICIT))
-def test_implicit_backward_vs_golden(golden, tag):
-    """LQRStep(no_op_forward=True) at the reference's fp64 solution; backward
+def implicit_file(tag, prec="f64"):
+    return f"implicit25_{prec}" if tag.startswith("cart25") else f"implicit_{prec}"
+
+
+@pytest.mark.parametrize("tag,prec", [(t, "f64") for t in IMPLICIT] +
+                         [(t, "f32") for t in IMPLICIT if t.startswith("cart25")])
+def test_implicit_backward_vs_golden(golden, tag, prec):
+    """LQRStep(no_op_forward=True) at the reference's solution; backward
     through the fused implicit kernel vs the reference's dC, dc, dtheta.
     Tolerance 1e-4 of the max magnitude (the reference's own fp32 result is
-    within ~3e-5 of its fp64 result, see tests/golden)."""
+    within ~3e-5 of its fp64 result, see tests/golden).  The T=25 cases are
+    also checked against the reference's own fp32 run (its fp32 MPC solution
+    and fp32 gradients, lqr_step_explicit.py:653-712).  There dtheta (from
+    torch.linalg.solve, :570) is always compared; dC and dc come from the
+    reference's fp32 lstsq on the 150x150 KKT matrix (:578, :585), which for the
+    unconstrained T=25 problems departs from the reference's OWN fp64 result by
+    0.98 (dC) and 0.74 (dc) of the max magnitude (the box-10 case: 1e-5) — so
+    the fp32 dC, dc goldens are compared only where the reference's fp32 agrees
+    with its fp64 to 1e-4 (the fp64 cases hold dC, dc for every tag)."""
     import dilqr
-    g = golden("implicit_f64")
+    g = golden(implicit_file(tag, prec))
+    g64 = golden(implicit_file(tag, "f64"))
     mname, bounds = IMPLICIT[tag]
     dx = dilqr_models()[mname]()
     x, u, Q, P, F, f, x0 = (gpu(g[f"{tag}_{k}"]) for k in ("x", "u", "Q", "P", "F", "f", "x0"))
@@ -754,8 +784,13 @@ def test_implicit_backward_vs_golden(golden, tag):
     loss = (x2 * gpu(g[f"{tag}_wx"])).sum() + (u2 * gpu(g[f"{tag}_wu"])).sum()
     loss.backward()
     assert relerr(cpu(theta.grad), g[f"{tag}_dtheta"]) < 1e-4
-    assert relerr(cpu(Qg.grad), g[f"{tag}_dQ"]) < 1e-4
-    assert relerr(cpu(Pg.grad), g[f"{tag}_dP"]) < 1e-4
+    ref_self = max(relerr(g[f"{tag}_dQ"], g64[f"{tag}_dQ"]), relerr(g[f"{tag}_dP"], g64[f"{tag}_dP"]))
+    if prec == "f64" or ref_self < 1e-4:
+        assert relerr(cpu(Qg.grad), g[f"{tag}_dQ"]) < 1e-4
+        assert relerr(cpu(Pg.grad), g[f"{tag}_dP"]) < 1e-4
+    else:
+        print(f"\n[{tag} f32] reference fp32 dC/dc off its own fp64 by {ref_self:.2f}: ours "
+              f"{relerr(cpu(Qg.grad), g[f'{tag}_dQ']):.2e} / {relerr(cpu(Pg.grad), g[f'{tag}_dP']):.2e} from its fp32")
     # per-problem dtheta straight from the kernel
     from dilqr import ops
     from dilqr.implicit import implicit_backward
@@ -790,7 +825,10 @@ def test_mpc_end_to_end_gradient(golden):
 
 def test_implicit_backward_full_size():
     """Config 4 shape (cartpole T=25, B=65536, bounds +-10): finite gradients,
-    and a 128-problem slice gives bit-identical per-problem results."""
+    a 128-problem slice gives bit-identical per-problem results, and an
+    8-problem slice matches the fp64 oracle's fast algebra run on the same fp32
+    solution (1e-4 of the max magnitude; oracle/adjoint.py is pinned to the
+    reference's T=25 gradients by test_oracle_golden.py[cart25_*])."""
     import dilqr
     from dilqr import ops
     from dilqr.implicit import implicit_backward
@@ -806,10 +844,22 @@ def test_implicit_backward_full_size():
     c = p.repeat(T, B, 1).to(DEV)
     wx = torch.randn(T, B, 5, device=DEV)
     wu = torch.randn(T, B, 1, device=DEV)
-    K, _, _ = ops.lqr_backward(C, c, None if T == 1 else ops.linearize(dx.model_id, ops.theta_of(dx, C), x, u)[0],
-                               5, 1, x=x, u=u, u_lower=-10.0, u_upper=10.0)
+    F = ops.linearize(dx.model_id, ops.theta_of(dx, C), x, u)[0]
+    K, _, _ = ops.lqr_backward(C, c, F, 5, 1, x=x, u=u, u_lower=-10.0, u_upper=10.0)
     dC, dc, dth = implicit_backward(dx, wx, wu, C, c, None, None, x, u, K, -10.0, 10.0, None)
     assert torch.isfinite(dC).all() and torch.isfinite(dc).all() and torch.isfinite(dth).all()
+    # an 8-problem slice spread over the batch (one problem from each of 8
+    # different waves) against the fp64 oracle on the same fp32 solution
+    so = [3, 8191, 16384, 20000, 33333, 47000, 60001, 65535]
+    f64 = lambda a: cpu(a[:, so]).astype(np.float64)  # noqa: E731
+    n_act = int(((u[:, so].abs() - 10.0).abs() <= 1e-8).sum())
+    rdC, rdc, rdth = oadj.implicit_backward_fast(omodels.Cartpole, f64(wx), f64(wu), f64(C), f64(c), f64(F), None,
+                                                 f64(x), f64(u), f64(K)[::-1].copy(), -10.0, 10.0)
+    print(f"\n[cartpole implicit full size] {n_act} active controls in the slice; vs fp64 oracle: dtheta "
+          f"{relerr(cpu(dth[so]), rdth):.2e}, dc {relerr(cpu(dc[:, so]), rdc):.2e}, dC {relerr(cpu(dC[:, so]), rdC):.2e}")
+    assert relerr(cpu(dth[so]), rdth) < 1e-4
+    assert relerr(cpu(dc[:, so]), rdc) < 1e-4
+    assert relerr(cpu(dC[:, so]), rdC) < 1e-4
     sl = slice(1000, 1128)
     dC2, dc2, dth2 = implicit_backward(dx, wx[:, sl].contiguous(), wu[:, sl].contiguous(), C[:, sl].contiguous(),
                                        c[:, sl].contiguous(), None, None, x[:, sl].contiguous(),
@@ -834,7 +884,7 @@ def test_implicit_backward_full_size():
     assert torch.equal(dth3, dth2) and torch.equal(dC3, dC2) and torch.equal(dc3, dc2)
 
 
-@pytest.mark.parametrize("tag", ["cart_unc", "cart_box", "pend_box"])
+@pytest.mark.parametrize("tag", ["cart_unc", "cart_box", "pend_box", "cart25_box10"])
 @pytest.mark.parametrize("cost", ["diag", "varying"])
 def test_implicit_backward_batch_independent(golden, tag, cost):
     """The golden problems tiled to B = 128 (two full waves) and 129 (a partial
@@ -844,7 +894,7 @@ def test_implicit_backward_batch_independent(golden, tag, cost):
     holding them in registers."""
     from dilqr import ops
     from dilqr.implicit import implicit_backward
-    g = golden("implicit_f64")
+    g = golden(implicit_file(tag))
     mname, bounds = IMPLICIT[tag]
     dx = dilqr_models()[mname]()
     x, u, Q, P, F, x0, wx, wu = (gpu(g[f"{tag}_{k}"]) for k in ("x", "u", "Q", "P", "F", "x0", "wx", "wu"))

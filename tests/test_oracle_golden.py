@@ -219,12 +219,19 @@ def test_classic_adjoint(golden, tag, bounds):
 # ---------------------------------------------------------------- DiLQR implicit backward
 IMPLICIT = {"cart_unc": ("cartpole", None), "cart_box": ("cartpole", (-5.0, 5.0)),
             "pend_box": ("pendulum", (-2.0, 2.0)), "rock_unc": ("rocket", None),
-            "rock_box": ("rocket", (-10.0, 10.0))}
+            "rock_box": ("rocket", (-10.0, 10.0)),
+            # config 4's horizon: cartpole T=25, B=8 (gen_golden.py IMPLICIT25_CASES)
+            "cart25_unc": ("cartpole", None), "cart25_box10": ("cartpole", (-10.0, 10.0)),
+            "cart25_box100": ("cartpole", (-100.0, 100.0))}
+
+
+def implicit_file(tag, prec="f64"):
+    return f"implicit25_{prec}" if tag.startswith("cart25") else f"implicit_{prec}"
 
 
 @pytest.mark.parametrize("tag", list(IMPLICIT))
 def test_implicit_backward_f64(golden, tag):
-    g = golden("implicit_f64")
+    g = golden(implicit_file(tag))
     mname, bounds = IMPLICIT[tag]
     M = MODELS[mname]
     x, u, Q, P, F = (g[f"{tag}_{k}"] for k in ("x", "u", "Q", "P", "F"))
@@ -262,3 +269,27 @@ def test_dataset_cartpole_known_answer(golden):
                                      max_linesearch_iter=int(g["cartpole_max_linesearch_iter"]))
     got = np.concatenate([x, u], 2).transpose(1, 0, 2)
     assert np.max(np.abs(got - tau)) < 5e-3
+
+
+@pytest.mark.parametrize("tag", list(IMPLICIT))
+def test_implicit_backward_fast_f64(golden, tag):
+    """The O(T d^3) algebra (the one the HIP kernels use, and the checker the
+    full-size GPU tests call) against the reference's (T d)^3 KKT solve."""
+    g = golden(implicit_file(tag))
+    mname, bounds = IMPLICIT[tag]
+    M = MODELS[mname]
+    x, u, Q, P = (g[f"{tag}_{k}"] for k in ("x", "u", "Q", "P"))
+    T, B, n = x.shape
+    m = u.shape[2]
+    Fo, fo = mpc.linearize(M, x, u)
+    lo, hi = bounds if bounds else (None, None)
+    K, _, _ = lqr.lqr_backward(Q, lqr.c_back(Q, P, x, u), Fo, n, m, u=u, u_lower=lo, u_upper=hi)
+    dC, dc, dth = adjoint.implicit_backward_fast(M, g[f"{tag}_wx"], g[f"{tag}_wu"], Q, P, Fo, fo, x, u,
+                                                 K[::-1], lo, hi)
+    # rocket: the reference's dense 160x160 KKT solve (lqr_step_explicit.py:570)
+    # is ill-conditioned enough to move its fp64 dtheta by ~6.5e-6 relative to
+    # the recursion's; every other case agrees to < 1e-6
+    tol = 2e-5 if mname == "rocket" else 1e-6
+    assert rel(dth, g[f"{tag}_dtheta_b"]) < tol
+    assert rel(dC, g[f"{tag}_dQ"]) < tol
+    assert rel(dc, g[f"{tag}_dP"]) < tol
