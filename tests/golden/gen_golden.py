@@ -514,6 +514,10 @@ IL_CASES = {
     "pend_sysid": ("pendulum", "sysid", False, True, 10, 5, 3, None),
     "pend_empc_dx": ("pendulum", "empc", False, True, 10, 5, 2, 30),
     "pend_empc_cost": ("pendulum", "empc", True, False, 10, 5, 2, 30),
+    # the north-star model's dataset (data/cartpole.pkl: 2 train / 1 val / 1 test
+    # trajectories, T=35, lqr_iter 100 from the dataset): n_batch 2 (the reference
+    # prints matrix_rank(A[1]), lqr_step_explicit.py:561, so a batch needs 2), 4 epochs
+    "cart_empc_dx": ("cartpole", "empc", False, True, 2, 2, 4, None),
 }
 
 
@@ -545,6 +549,9 @@ def case_il():
         for k in ("train_data", "val_data", "test_data"):
             setattr(env, k, torch.tensor(tensors[k], dtype=torch.float32))
         il_exp.pkl = types.SimpleNamespace(load=lambda f, _e=env: _e, dump=lambda *a, **k: None)
+        # MKL's multi-threaded getrf/laswp fails on the >100-wide KKT systems
+        # (T=35, d=6 -> 210) in this image (see case_implicit); one thread is fine
+        torch.set_num_threads(1 if ds == "cartpole" else 8)
         work = tempfile.mkdtemp()
         lin = R.mpc_explicit.MPC.linearize_dynamics
         if mode == "empc":

@@ -102,34 +102,44 @@ def test_il_golden_records_reference_behaviour(golden):
     g = golden("il")
     assert "pend_sysid_train" in g and "pend_sysid_dx_hist" in g
     for k in ("pend_empc_dx_train", "pend_empc_dx_val_test", "pend_empc_dx_dx_hist", "pend_empc_cost_train",
-              "pend_empc_cost_val_test", "pend_empc_cost_cost_hist"):
+              "pend_empc_cost_val_test", "pend_empc_cost_cost_hist", "cart_empc_dx_train", "cart_empc_dx_val_test",
+              "cart_empc_dx_dx_hist"):
         assert k in g and np.isfinite(g[k]).all(), k
     assert not any(k.endswith("_error") for k in g)
 
 
+# case: (dataset, lqr_iter override, n_batch, n_train, n_epoch) — gen_golden.py IL_CASES
+EMPC_CASES = {"pend_empc_dx": (PEND_PKL, 30, 5, 10, 2), "pend_empc_cost": (PEND_PKL, 30, 5, 10, 2),
+              "cart_empc_dx": (CART_PKL, None, 2, 2, 4)}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["pend_empc_dx", "pend_empc_cost"])
+@pytest.mark.parametrize("case", list(EMPC_CASES))
 def test_il_empc_matches_reference_curve(golden, case):
-    """ILTrainer(mode='empc') on data/pendulum.pkl (n_train=10, n_batch=5, 2
-    epochs, lqr_iter 30, seed 5) reproduces the reference IL_Exp.run's
+    """ILTrainer(mode='empc') reproduces the reference IL_Exp.run's
     train_losses.csv (im_loss through the MPC + the DiLQR implicit backward),
     val_test_losses.csv and dx_hist.csv / cost_hist.csv: the parameter steps
     are RMSprop steps on the implicit gradients, so the histories pin dtheta
-    (learn_dx) and dC, dc through q, p (learn_cost) end to end."""
+    (learn_dx) and dC, dc through q, p (learn_cost) end to end.  On
+    data/pendulum.pkl: n_train=10, n_batch=5, 2 epochs, lqr_iter 30, seed 5.
+    On data/cartpole.pkl (the north-star model, T=35, lqr_iter 100 from the
+    dataset, bounds +-100): its 2 training trajectories, n_batch=2, 4 epochs."""
     from dilqr import il
     g = golden("il")
-    env = il.IL_Env.from_dataset(PEND_PKL, device="cuda")
-    env.lqr_iter = 30
-    kw = {"learn_dx": True} if case == "pend_empc_dx" else {"learn_cost": True}
-    tr = il.ILTrainer(env, mode="empc", n_batch=5, n_train=10, seed=5, **kw)
-    h = tr.fit(2)
+    path, lqr_iter, n_batch, n_train, n_epoch = EMPC_CASES[case]
+    env = il.IL_Env.from_dataset(path, device="cuda")
+    if lqr_iter:
+        env.lqr_iter = lqr_iter
+    kw = {"learn_cost": True} if case.endswith("_cost") else {"learn_dx": True}
+    tr = il.ILTrainer(env, mode="empc", n_batch=n_batch, n_train=n_train, seed=5, **kw)
+    h = tr.fit(n_epoch)
     train = np.array(h["train"])
     ref = g[f"{case}_train"]
     print(f"{case}: train {train.tolist()}\n  ref {ref.tolist()}")
     assert train.shape == ref.shape
     np.testing.assert_allclose(train[:, 0], ref[:, 0])
     np.testing.assert_allclose(train[:, 1:], ref[:, 1:], rtol=2e-3, atol=1e-5)
-    if case == "pend_empc_dx":
+    if "learn_dx" in kw:
         hist, ghist = np.array(h["params"]), g[f"{case}_dx_hist"][1:]
     else:
         hist, ghist = np.array(h["cost"]), g[f"{case}_cost_hist"][1:]
