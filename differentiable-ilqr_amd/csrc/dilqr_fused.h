@@ -1170,7 +1170,7 @@ __global__ void __launch_bounds__(kSmallMax) k_mpc_solve_small(int T, int B, con
     imp = 1;
   }
   int done = 0, n_not_improved = 0, stopped = 0;
-  unsigned mx_all = 0u;
+  unsigned mx_all = 0u, mx_prev = 0u;
   for (;;) {
     ++done;
     __syncthreads();                                       // every lane's du rows of this iteration are stored
@@ -1197,6 +1197,7 @@ __global__ void __launch_bounds__(kSmallMax) k_mpc_solve_small(int T, int B, con
     mx = 0u;
     any = 0;
     for (int i = 0; i < nw; ++i) { mx = red_max[i] > mx ? red_max[i] : mx; any |= red_any[i]; }
+    mx_prev = mx_all;
     mx_all = mx;
     if (done == iters) break;                              // the last iteration's rule is never applied
     n_not_improved = any ? 0 : n_not_improved + 1;         // mpc_explicit.py:264, 279 (mpc_decide)
@@ -1222,11 +1223,16 @@ __global__ void __launch_bounds__(kSmallMax) k_mpc_solve_small(int T, int B, con
     S.improved[b] = imp;
   }
   if (b == 0) {
+    // the control word the per-iteration launches leave: a stop is published by
+    // the prologue of the iteration after the one that met the rule (iter =
+    // iterations that ran, that iteration's max); without a stop the last
+    // prologue ran before the last iteration (iter = iters - 1, the max of the
+    // iteration before it)
     dilqr_mpc_ctrl o = {};
-    o.iter = done;
+    o.iter = stopped ? done : done - 1;
     o.stopped = stopped;
     o.n_not_improved = n_not_improved;
-    o.max_du_bits = mx_all;
+    o.max_du_bits = stopped ? mx_all : mx_prev;
     S.ctrl[0] = o;
     S.ctrl[1] = o;
   }

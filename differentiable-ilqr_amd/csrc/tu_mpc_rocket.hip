@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(64, MODE == GAIN_BOX ? 2 : DCONST ? DILQR_SWEE
   const bool first = iteration == 0;
   // the dense-cost instantiation after iteration 0, when iteration 0 found
   // every cost to be a time-invariant diagonal one: nothing to do (it is
-  // launched on a small grid then, kDenseGrid8, so an empty pass costs little)
+  // launched on a grid capped at the chip's resident workgroups then, striding)
   if (!DCONST && !first && S.Cpk && S.done_counter[kDenseCount] == 0u) return;
   const int l = threadIdx.x & (kG8 - 1), gp = threadIdx.x / kG8;
   Model md; md.load(theta);
@@ -129,11 +129,22 @@ __global__ void __launch_bounds__(64, MODE == GAIN_BOX ? 2 : DCONST ? DILQR_SWEE
 #ifndef DILQR_SWEEP_LANES
 #define DILQR_SWEEP_LANES 8
 #endif
-// workgroups of a dense-cost launch that usually finds nothing to do
-#ifndef DILQR_DENSE_GRID
-#define DILQR_DENSE_GRID 256
-#endif
-constexpr int kDenseGrid = DILQR_DENSE_GRID;
+// The dense-cost instantiations after iteration 0 usually find nothing to do
+// (iteration 0 counted no dense-cost problem), but the host cannot see that
+// count without a sync, so their grid must serve a batch of dense costs at full
+// speed too: it is capped at the workgroups the chip keeps resident at once
+// (CUs x the kernel's occupancy per CU), and the kernel strides over the rest.
+// (Round 5 capped it at 256 workgroups, which left a dense batch at a quarter
+// of a wave per SIMD, striding serially — ADVICE r05.)
+template <class K>
+int resident_workgroups(K kern, int threads, size_t lds) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, lds) != hipSuccess || cus <= 0 || per <= 0)
+    return 1 << 30;                                       // unknown: no cap
+  return cus * per;
+}
 
 // DILQR_SEARCH_QUAD: the line search on a quad of lanes per problem (1, the
 // default: every pass of a round at once, cost only) or on lane pairs (0)
@@ -143,10 +154,13 @@ constexpr int kDenseGrid = DILQR_DENSE_GRID;
 int launch_mpc_step_rocket(const MpcStepArgs& a) {
 #if DILQR_SEARCH_QUAD
   const int gq = grid_for(4 * (long long)a.B);
-  const int gq_dense = a.st.Cpk ? (gq < kDenseGrid ? gq : kDenseGrid) : gq;
 #define SEARCH(BM_, DC_)                                                                                          \
-  k_mpc_search_quad<Rocket, BM_, DC_><<<DC_ ? gq : gq_dense, kBlock, 0, a.stream>>>(                             \
-      a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st)
+  do {                                                                                                            \
+    static const int cap = resident_workgroups(k_mpc_search_quad<Rocket, BM_, false>, kBlock, 0);                 \
+    const int g = (DC_ || !a.st.Cpk) ? gq : (gq < cap ? gq : cap);                                                 \
+    k_mpc_search_quad<Rocket, BM_, DC_><<<g, kBlock, 0, a.stream>>>(                                               \
+        a.T, a.B, a.theta, a.x_init, a.C, a.c, a.bd, a.decay, a.max_ls, a.iteration, a.best_cost_eps, a.G, a.st);  \
+  } while (0)
 #else
 #define SEARCH(BM_, DC_)                                                                                          \
   k_mpc_search_lane<Rocket, BM_, DC_><<<grid_for(2 * (long long)a.B), kBlock, 0, a.stream>>>(                     \
@@ -158,10 +172,13 @@ int launch_mpc_step_rocket(const MpcStepArgs& a) {
   // (every cost a time-invariant diagonal one) costs a few workgroups, not
   // B/8 of them
   const int g8 = (int)((a.B + kG8PW - 1) / kG8PW);
-  const int g8_dense = (a.iteration > 0 && a.st.Cpk) ? (g8 < kDenseGrid ? g8 : kDenseGrid) : g8;
 #define SWEEP8(MODE_, DC_)                                                                                        \
-  k_mpc_sweep_g8<Rocket, MODE_, DC_><<<DC_ ? g8 : g8_dense, 64, 0, a.stream>>>(                                   \
-      a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration, a.eps, a.lim, a.G, a.st)
+  do {                                                                                                            \
+    static const int cap = resident_workgroups(k_mpc_sweep_g8<Rocket, MODE_, false>, 64, 0);                      \
+    const int g = (DC_ || a.iteration == 0 || !a.st.Cpk) ? g8 : (g8 < cap ? g8 : cap);                           \
+    k_mpc_sweep_g8<Rocket, MODE_, DC_><<<g, 64, 0, a.stream>>>(a.T, a.B, a.theta, a.C, a.c, a.bd, a.iteration,    \
+                                                              a.eps, a.lim, a.G, a.st);                           \
+  } while (0)
 #define SWEEP(MODE_)                                                                                              \
   SWEEP8(MODE_, true);                                                                                            \
   SWEEP8(MODE_, false)

@@ -361,7 +361,14 @@ class MPCSolve:
 
     @property
     def iterations(self):
-        return int(self._ctrl_now()[0].item())
+        """The iterations that ran: the device's count when the stop rule fired
+        (published by the prologue after the iteration that met it), else every
+        launched iteration (the rule of the last one is never applied, so the
+        device word then reads one less; every solve path leaves the same word)."""
+        ctrl = self._ctrl_now()
+        if int(ctrl[1].item()):
+            return int(ctrl[0].item())
+        return self.last_iteration + 1
 
 
 # dilqr_mpc_solve_small_f32: batches one workgroup holds, thread-per-problem models
@@ -460,9 +467,7 @@ def _mpc_solve_logged(sv, model_id, theta, x_init, C, c, u_init, bounds, unbound
     # the iterations that ran: the rule after iteration k is applied by
     # iteration k+1's prologue, which then publishes iter = k+1 with the stop
     # flag (dilqr_fused.h mpc_decide); a solve that never stopped ran them all
-    ran = lqr_iter
-    if not sv.fixed_iters and lqr_iter > 1 and sv.stopped:
-        ran = sv.iterations
+    ran = sv.iterations
     # total_qp_iters: 0 without bounds, as the reference (pnqp runs only with
     # bounds, lqr_step_explicit.py:137-150); the fused kernels do not count the
     # batch-coupled pnqp iterations the reference reports with bounds

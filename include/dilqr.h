@@ -383,8 +383,11 @@ int dilqr_mpc_solve_fixed_f32(int model, int T, int B, const float* theta, const
    problem — the rule's batch-mixing rows and reductions need a barrier, not a
    launch, and the host polls nothing.  The same iterates, costs, best_du,
    full_du_norm and stop iteration as dilqr_mpc_begin_f32 +
-   dilqr_mpc_iterate_f32 per iteration; ctrl[0] = ctrl[1] = {iterations run,
-   stopped, n_not_improved, max_du_bits}.  B <= 256 and the thread-per-problem
+   dilqr_mpc_iterate_f32 per iteration; ctrl[0] = ctrl[1] = the control word
+   those launches leave: {iter, stopped, n_not_improved, max_du_bits} with iter
+   = the iterations run and max_du_bits that of the last one when the rule
+   stopped the solve, else iter = iterations - 1 and the max of the iteration
+   before the last (the last iteration's rule is never applied).  B <= 256 and the thread-per-problem
    models (pendulum, cartpole, 5-parameter pendulum); DILQR_E_SHAPE otherwise.
    Replaces the per-iteration loop of MPC.forward for the IL loop's batches
    (il_exp.py:44 n_batch = 32, il_env.py:153-188). */

@@ -229,10 +229,13 @@ def test_small_batch_solve_equals_per_iteration_launches(model, B, bounds, eps, 
     b.begin(dx.model_id, th_, x0)
     for i in range(iters):
         b.iterate(dx.model_id, th_, x0, C, c, nb, decay, mls, i, 1e-4, eps, lim)
-    ran_b = b.iterations if b.stopped else iters
-    print(f"{model} B={B}: small solve ran {a.iterations} (stopped {a.stopped}), per-iteration {ran_b} "
+    print(f"{model} B={B}: small solve ran {a.iterations} (stopped {a.stopped}), per-iteration {b.iterations} "
           f"(stopped {b.stopped})")
-    assert a.iterations == ran_b and a.stopped == b.stopped
+    assert a.iterations == b.iterations and a.stopped == b.stopped
+    assert b.stopped or b.iterations == iters
+    # the control word itself (iter, stopped, n_not_improved, max) is the same,
+    # stopped or not
+    assert torch.equal(a._ctrl_now(), b._ctrl_now())
     xa, ua = a.gather_best()
     xb, ub = b.gather_best()
     assert torch.equal(xa, xb) and torch.equal(ua, ub)
@@ -298,7 +301,9 @@ def test_small_batch_solve_edges(B, T, iters, mls):
     b.begin(dx.model_id, th_, x0)
     for i in range(iters):
         b.iterate(dx.model_id, th_, x0, C, c, nb, 0.5, mls, i, 1e-4, 1e-3, 2)
-    assert a.iterations == (b.iterations if b.stopped else iters) and a.stopped == b.stopped
+    assert a.iterations == b.iterations and a.stopped == b.stopped
+    assert b.stopped or b.iterations == iters
+    assert torch.equal(a._ctrl_now(), b._ctrl_now())
     xa, ua = a.gather_best()
     xb, ub = b.gather_best()
     assert torch.equal(xa, xb) and torch.equal(ua, ub)

@@ -56,6 +56,15 @@ extern "C" void MODEL##_f_theta_cs(const float* th, const float* x, const float*
 }
 WRAP(Pendulum, 4, 3, 1, 3)
 WRAP(Cartpole, 6, 5, 1, 4)
+#define WRAPCS(MODEL, N, M)                                                                    \
+extern "C" void MODEL##_next_cs(const float* th, const float* x, const float* u, float* out) { \
+  float xx[N], uu[M];                                                                          \
+  for (int i = 0; i < N; ++i) xx[i] = x[i];                                                    \
+  for (int i = 0; i < M; ++i) uu[i] = u[i];                                                    \
+  dilqr::gen::MODEL##D2::next_cs(th, xx, uu, out[0], out[1]);                                  \
+}
+WRAPCS(Pendulum, 3, 1)
+WRAPCS(Cartpole, 5, 1)
 // get_matrices' second-order pieces (the caller zero-fills, as the kernel does)
 #define WRAPM(MODEL, N, M)                                                                     \
 extern "C" void MODEL##_matrices(const float* th, const float* x, const float* u, float* Dp,   \
@@ -190,3 +199,47 @@ def test_generated_get_matrices_vs_reference(shim, golden, name):
         for got, key in ((Dp, "D_params"), (Dx, "D_x"), (Du, "D_u"), (xth, "x_theta"), (xx, "x_xtm1")):
             ref = g[f"{name}_gm_{key}"][b]
             assert np.abs(got - ref).max() / scale(ref) < 2e-4, (name, key, b, np.abs(got - ref).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pendulum", "cartpole"])
+def test_device_next_cs_matches_generated(shim, name):
+    """The implicit backward feeds the generated second-order pieces
+    (gen::*D2::lag_hess / lag_dparam / f_theta_cs) the cos/sin of the integrated
+    angle from the device model's Model::next_cs (angle_step, no atan2), where
+    the host tests above pair them with gen::*D2::next_cs (atan2f/cosf/sinf).
+    The two conventions must agree — including controls beyond the torque limit,
+    where the pendulum's pair is formed at the UNCLAMPED u (pendulum.py:444-475)
+    and differs from the next state's.  Model::next_cs is read back through the
+    device Jacobian's rows that scale it by dt (pendulum D[0][2] = -sn dt,
+    D[1][2] = cs dt; cartpole D[2][4] = -sn dt, D[3][4] = cs dt) and, for the
+    cartpole (u-independent), also from the next state (x'[2], x'[3])."""
+    import torch
+    from dilqr.env_dx.cartpole import CartpoleDx
+    from dilqr.env_dx.pendulum import PendulumDx
+    dx = PendulumDx() if name == "pendulum" else CartpoleDx()
+    rng = np.random.RandomState(11)
+    N = 256
+    th = rng.uniform(-np.pi, np.pi, N)
+    if name == "pendulum":
+        x = np.stack([np.cos(th), np.sin(th), rng.uniform(-8, 8, N)], 1)
+        u = rng.uniform(-6, 6, (N, 1))                    # half of them beyond +-2
+        dt, (ri, rj), col = 0.05, (0, 1), 2
+    else:
+        x = np.stack([rng.uniform(-1, 1, N), rng.uniform(-2, 2, N), np.cos(th), np.sin(th),
+                      rng.uniform(-8, 8, N)], 1)
+        u = rng.uniform(-300, 300, (N, 1))                # beyond +-100
+        dt, (ri, rj), col = 0.05, (2, 3), 4
+    x32, u32 = x.astype(np.float32), u.astype(np.float32)
+    xg = torch.tensor(x32, device="cuda")
+    ug = torch.tensor(u32, device="cuda")
+    D = dx.get_linear_dyn(xg, ug).cpu().numpy().astype(np.float64)
+    sn_dev, cs_dev = -D[:, ri, col] / dt, D[:, rj, col] / dt
+    thp = np.array(dx.params.detach().cpu().numpy(), np.float32)
+    gen = np.stack([call(shim, f"{name.capitalize()}_next_cs", thp, x32[b], u32[b], out_size=2) for b in range(N)])
+    err = max(np.abs(cs_dev - gen[:, 0]).max(), np.abs(sn_dev - gen[:, 1]).max())
+    print(f"\n[{name}] device next_cs vs generated next_cs: max abs {err:.2e}")
+    assert err < 2e-6
+    if name == "cartpole":
+        xn = dx(xg, ug).cpu().numpy()
+        assert np.abs(xn[:, 2:4] - gen).max() < 2e-6
