@@ -60,6 +60,58 @@ DEV void costate_step(const float (&Ct)[n + m][n + m], const float (&cx)[n], con
   for (int i = 0; i < n; ++i) lam[i] = nl[i];
 }
 
+// DILQR_IMPL_SKIP: timing-only builds (tools/ab.sh variants, never the shipped
+// library) that leave out pass C (bit 0) and/or pass D (bit 1), to split the
+// kernel's time by pass as rocket's group kernel does, or pass D's generated
+// pieces (bit 2 lag_hess, bit 3 lag_dparam, bit 4 f_theta_cs: zeros instead)
+#ifndef DILQR_IMPL_SKIP
+#define DILQR_IMPL_SKIP 0
+#endif
+
+// One wave's records of K floats for problems b0 .. b0+63 of one step are one
+// contiguous run of 64*K floats ([t, b, K] layout).  Each lane writes its record
+// to LDS and the wave stores the run coalesced (a 1-KiB dwordx4 run per
+// instruction) instead of each lane storing its own 144-byte record: per-lane
+// record stores ran at half the HBM write rate of coalesced ones
+// (tools/microbench/store_patterns.hip).  One wave per workgroup
+// (kBlock = 64): its LDS accesses complete in program order, so the wave
+// barriers (scheduling only) are the whole synchronisation.  Lane strides of K
+// dwords (K/4 float4, K/2 float2) keep the b128 / b64 writes bank-conflict free
+// for the K used here (16, 36; 4, 6).
+template <int K>
+DEV void wave_store_records(float* __restrict__ base, const float (&r)[K], float* __restrict__ lds, int lane,
+                            int nvalid) {
+  static_assert(K % 2 == 0, "records of an even number of floats");
+  __builtin_amdgcn_wave_barrier();                 // the previous step's reads of lds precede these writes
+  if constexpr (K % 4 == 0) {
+    constexpr int Q = K / 4;
+    float4* L = reinterpret_cast<float4*>(lds);
+#pragma unroll
+    for (int i = 0; i < Q; ++i) L[lane * Q + i] = make_float4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+    __builtin_amdgcn_wave_barrier();
+    float4* g = reinterpret_cast<float4*>(base);
+    const int nv = nvalid * Q;
+#pragma unroll
+    for (int j = 0; j < Q; ++j) {
+      const int i = lane + 64 * j;
+      if (i < nv) g[i] = L[i];
+    }
+  } else {
+    constexpr int Q = K / 2;
+    float2* L = reinterpret_cast<float2*>(lds);
+#pragma unroll
+    for (int i = 0; i < Q; ++i) L[lane * Q + i] = make_float2(r[2 * i], r[2 * i + 1]);
+    __builtin_amdgcn_wave_barrier();
+    float2* g = reinterpret_cast<float2*>(base);
+    const int nv = nvalid * Q;
+#pragma unroll
+    for (int j = 0; j < Q; ++j) {
+      const int i = lane + 64 * j;
+      if (i < nv) g[i] = L[i];
+    }
+  }
+}
+
 template <class Model>
 __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     int T, int B, const float* __restrict__ theta, const float* __restrict__ C, const float* __restrict__ c,
@@ -69,8 +121,14 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
   using D2 = typename D2Of<Model>::type;
   using W = ImplicitWs<Model>;
   constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m, G = W::G;
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  // every lane of the wave runs (pass D stores the wave's dC, dc records
+  // together); lanes past the batch shadow problem B-1 and store nothing
+  const int lane = threadIdx.x, b0 = blockIdx.x * kBlock;
+  const int nvalid = B - b0 < kBlock ? B - b0 : kBlock;
+  const bool valid = lane < nvalid;
+  const int b = valid ? b0 + lane : B - 1;
+  __shared__ __attribute__((aligned(16))) float s_dC[kBlock * d * d];
+  __shared__ __attribute__((aligned(16))) float s_dc[kBlock * d];
   Model md; md.load(theta);
   float* const wsG = ws;
   float* const wsY = ws + W::y_off(T, B);
@@ -151,7 +209,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         for (int j = 0; j < n; ++j) gr[a * n + j] = Kt[a][j];
         gr[m * n + a] = kt[a];
       }
-      SoaRec<G>::store(wsG, gr, T, t, B, b);
+      if (valid) SoaRec<G>::store(wsG, gr, T, t, B, b);
       float cx[n];
 #pragma unroll
       for (int i = 0; i < n; ++i) cx[i] = ct[i];
@@ -165,7 +223,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     float yx[n];
 #pragma unroll
     for (int i = 0; i < n; ++i) yx[i] = 0.f;
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < ((DILQR_IMPL_SKIP & 1) ? 0 : T); ++t) {
       size_t tb = (size_t)t * B + b;
       float xt[n], ut[m], gr[G];
       ld(xt, x + tb * n); ld(ut, u + tb * m);
@@ -180,7 +238,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         for (int j = 0; j < n; ++j) s_ += gr[a * n + j] * yx[j];
         y[n + a] = active(tb, a, ut[a]) ? 0.f : (s_ + 0.f) + gr[m * n + a];
       }
-      SoaRec<d>::store(wsY, y, T, t, B, b);
+      if (valid) SoaRec<d>::store(wsY, y, T, t, B, b);
       if (t < T - 1) {
         float D[n][d];
         md.jacobian(xt, ut, D);
@@ -203,7 +261,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     for (int a = 0; a < m; ++a) au[a] = 0.f;
 #pragma unroll
     for (int k = 0; k < p; ++k) dth[k] = 0.f;
-    for (int t = T - 1; t >= 0; --t) {
+    for (int t = (DILQR_IMPL_SKIP & 2) ? -1 : T - 1; t >= 0; --t) {
       size_t tb = (size_t)t * B + b;
       float Ct[d][d], ct[d], xt[n], ut[m], gxx[n], gu[m], y[d];
       if (c_regs) {
@@ -236,8 +294,9 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         for (int j = 0; j < d; ++j) dCt[i][j] = -0.5f * (y[i] * tau[j] + tau[i] * y[j]);
         dct[i] = -y[i];
       }
-      st2(dC + tb * d * d, dCt);
-      st(dc + tb * d, dct);
+      wave_store_records<d * d>(dC + ((size_t)t * B + b0) * d * d,
+                                *reinterpret_cast<const float(*)[d * d]>(&dCt[0][0]), s_dC, lane, nvalid);
+      wave_store_records<d>(dc + ((size_t)t * B + b0) * d, dct, s_dc, lane, nvalid);
       float D[n][d], wx[n], hx[n], cn, sn;
       md.next_cs(xt, ut, cn, sn);         // the integrated angle, once per step
       md.jacobian_sc(xt, ut, cn, sn, D);  // D_t (t = T-1: only for A_{T-1} of the mu carry)
@@ -246,8 +305,22 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       if (t < T - 1) {
         float Kq[m][n], Mt[d][d], Mp[d][p];
         ld2(Kq, K + ((size_t)(T - 1 - t) * B + b) * m * n);
+#if DILQR_IMPL_SKIP & 4
+#pragma unroll
+        for (int i = 0; i < d; ++i)
+#pragma unroll
+          for (int j = 0; j < d; ++j) Mt[i][j] = 0.f;
+#else
         D2::lag_hess(theta, xt, ut, lam, cn, sn, Mt);  // lam = lam_{t+1}
+#endif
+#if DILQR_IMPL_SKIP & 8
+#pragma unroll
+        for (int i = 0; i < d; ++i)
+#pragma unroll
+          for (int j = 0; j < p; ++j) Mp[i][j] = 0.f;
+#else
         D2::lag_dparam(theta, xt, ut, lam, cn, sn, Mp);
+#endif
         // w_t = g_t - M_t^T y_t
 #pragma unroll
         for (int k = 0; k < n; ++k) {
@@ -332,7 +405,14 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
 #pragma unroll
         for (int l = 0; l < n; ++l) mu[l] = hx[l] - dlam[l];
         float ft[n][p];
+#if DILQR_IMPL_SKIP & 16
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int j = 0; j < p; ++j) ft[i][j] = 0.f;
+#else
         D2::f_theta_cs(theta, xt, ut, cn, sn, ft);
+#endif
 #pragma unroll
         for (int k = 0; k < p; ++k) {
           float s = 0.f;
@@ -358,7 +438,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         }
       }
     }
-    st(dtheta + (size_t)b * p, dth);
+    if (valid) st(dtheta + (size_t)b * p, dth);
   }
 }
 

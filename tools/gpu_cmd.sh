@@ -1,4 +1,12 @@
+#!/usr/bin/env bash
+# round-6 scratch GPU session: implicit tests on the in-tree library, then A/B of ab/ variants
 set -o pipefail
-PYTEST_K="small_batch or next_cs or rocket or dense" bash tools/gpu_session_r05.sh || exit 1
-AB_CMD=tools/ab_rocket_dense.py timeout -k 10 600 bash tools/ab.sh 3 > gpurun_out/ab_dense.txt 2>&1; rc=$?
-cat gpurun_out/ab_dense.txt; exit $rc
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+if [ "${PYTEST:-1}" = 1 ]; then
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -k "${PYTEST_K:-implicit or end_to_end or il_}" \
+    > gpurun_out/pytest_implicit.log 2>&1; rc=$?
+tail -3 gpurun_out/pytest_implicit.log; [ $rc -eq 0 ] || exit $rc
+fi
+AB_CMD="${AB_CMD:-tools/ab_implicit.py}" timeout -k 10 600 bash tools/ab.sh ${AB_ROUNDS:-3} > gpurun_out/ab.txt 2>&1; rc=$?
+grep -v amdgpu.ids gpurun_out/ab.txt; exit $rc

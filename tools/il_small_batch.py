@@ -57,8 +57,20 @@ def measure(B, reps=5, dev=torch.device("cuda", 0)):
 
 
 if __name__ == "__main__":
+    # --both: each batch size on the one-launch small-batch solve AND on the
+    # per-iteration launches (ops.SMALL_BATCH_MAX set to 0 for the latter), to
+    # place SMALL_BATCH_MAX
+    from dilqr import ops
+    both = "--both" in sys.argv
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
-        sizes = [int(a) for a in sys.argv[1:]] or [32, 4096]
-        out = [measure(B) for B in sizes]
+        sizes = [int(a) for a in sys.argv[1:] if not a.startswith("--")] or [32, 4096]
+        out = []
+        keep = ops.SMALL_BATCH_MAX
+        for B in sizes:
+            out.append(measure(B))
+            if both and B <= keep:
+                ops.SMALL_BATCH_MAX = 0
+                out.append(measure(B))
+                ops.SMALL_BATCH_MAX = keep
     print(json.dumps(out), flush=True)
