@@ -238,13 +238,22 @@ struct Cartpole {
 }  // namespace dilqr
 
 #include "dilqr_models_gen.h"
+#include "dilqr_d2_sparsity.h"
 
 namespace dilqr {
 // Second-order terms of each model for the implicit backward.  XX00_ZERO: the
 // reference's x_grad_xtm1 has a 0 where d x_{t+1}/d x_t is 1 (cartpole.py:666).
+// hess_nz / dparam_nz / ftheta_nz (dilqr_d2_sparsity.h): the generated
+// pieces' structural zeros, skipped by the implicit backward at compile time.
 template <class Model> struct D2Of;
-template <> struct D2Of<Pendulum> { using type = gen::PendulumD2; static constexpr bool XX00_ZERO = false; };
-template <> struct D2Of<Cartpole> { using type = gen::CartpoleD2; static constexpr bool XX00_ZERO = true; };
+template <> struct D2Of<Pendulum> : gen::PendulumD2Z {
+  using type = gen::PendulumD2;
+  static constexpr bool XX00_ZERO = false;
+};
+template <> struct D2Of<Cartpole> : gen::CartpoleD2Z {
+  using type = gen::CartpoleD2;
+  static constexpr bool XX00_ZERO = true;
+};
 }  // namespace dilqr
 
 namespace dilqr {

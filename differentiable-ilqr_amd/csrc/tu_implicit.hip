@@ -40,7 +40,7 @@ template <class Model> struct ImplicitWs {
 // lam_t = Cxx x + Cxu u + c_x + F_x^T lam_{t+1}   (lqr_step_explicit.py:305-319);
 // D is zero at t = T-1.  Passes B and D run this same function on the same
 // inputs, so they hold the same bits.
-template <int n, int m>
+template <int n, int m, class FS = DenseF>
 DEV void costate_step(const float (&Ct)[n + m][n + m], const float (&cx)[n], const float (&xt)[n],
                       const float (&ut)[m], const float (&D)[n][n + m], float (&lam)[n]) {
   float nl[n];
@@ -53,7 +53,8 @@ DEV void costate_step(const float (&Ct)[n + m][n + m], const float (&cx)[n], con
     for (int a = 0; a < m; ++a) s2 += Ct[i][n + a] * ut[a];
     float s3 = 0.f;
 #pragma unroll
-    for (int l = 0; l < n; ++l) s3 += D[l][i] * lam[l];
+    for (int l = 0; l < n; ++l)
+      if (FS::nz(l, i)) s3 += D[l][i] * lam[l];
     nl[i] = ((s + s2) + cx[i]) + s3;
   }
 #pragma unroll
@@ -66,6 +67,15 @@ DEV void costate_step(const float (&Ct)[n + m][n + m], const float (&cx)[n], con
 // pieces (bit 2 lag_hess, bit 3 lag_dparam, bit 4 f_theta_cs: zeros instead)
 #ifndef DILQR_IMPL_SKIP
 #define DILQR_IMPL_SKIP 0
+#endif
+#ifndef DILQR_IMPL_PFD
+#define DILQR_IMPL_PFD 1
+#endif
+#ifndef DILQR_IMPL_PFB
+#define DILQR_IMPL_PFB 1
+#endif
+#ifndef DILQR_IMPL_PFC
+#define DILQR_IMPL_PFC 0
 #endif
 
 // One wave's records of K floats for problems b0 .. b0+63 of one step are one
@@ -119,6 +129,8 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     const float* __restrict__ dl_dx, const float* __restrict__ dl_du, Bounds bd, float* __restrict__ ws,
     float* __restrict__ dC, float* __restrict__ dc, float* __restrict__ dtheta) {
   using D2 = typename D2Of<Model>::type;
+  using DZ = D2Of<Model>;                          // structural zeros of the generated pieces
+  using FS = typename Model::FSparsity;            // ... and of the Jacobian
   using W = ImplicitWs<Model>;
   constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m, G = W::G;
   // every lane of the wave runs (pass D stores the wave's dC, dc records
@@ -156,11 +168,51 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     float lam[n];
 #pragma unroll
     for (int i = 0; i < n; ++i) lam[i] = 0.f;
+#if DILQR_IMPL_PFB
+    // step t-1's x, u and loss gradients loaded while step t computes (1, the
+    // shipped setting: config 4 0.220 -> 0.207 ms; 2, C_t and c_t too: 28
+    // AGPRs, 0.213 ms — profiles/r06/ab_implicit_cartpole_prefetch.txt)
+    struct BIn {
+      float x[n], u[m], gx[n], gu[m];
+#if DILQR_IMPL_PFB > 1
+      float C[d][d], c[d];
+#endif
+    };
+    auto load_b = [&](int t, BIn& in) {
+      const size_t tb = (size_t)t * B + b;
+      ld(in.x, x + tb * n); ld(in.u, u + tb * m); ld(in.gx, dl_dx + tb * n); ld(in.gu, dl_du + tb * m);
+#if DILQR_IMPL_PFB > 1
+      ld2(in.C, C + tb * d * d); ld(in.c, c + tb * d);
+#endif
+    };
+    BIn bin;
+    load_b(T - 1, bin);
+#endif
     for (int t = T - 1; t >= 0; --t) {
       size_t tb = (size_t)t * B + b;
       float Ct[d][d], ct[d], xt[n], ut[m], gxx[n], gu[m];
+#if DILQR_IMPL_PFB
+      BIn bnx;
+      load_b(t > 0 ? t - 1 : 0, bnx);
+#pragma unroll
+      for (int i = 0; i < n; ++i) { xt[i] = bin.x[i]; gxx[i] = bin.gx[i]; }
+#pragma unroll
+      for (int a = 0; a < m; ++a) { ut[a] = bin.u[a]; gu[a] = bin.gu[a]; }
+#if DILQR_IMPL_PFB > 1
+#pragma unroll
+      for (int i = 0; i < d; ++i) {
+        ct[i] = bin.c[i];
+#pragma unroll
+        for (int j = 0; j < d; ++j) Ct[i][j] = bin.C[i][j];
+      }
+#else
+      ld2(Ct, C + tb * d * d); ld(ct, c + tb * d);
+#endif
+      bin = bnx;
+#else
       ld2(Ct, C + tb * d * d); ld(ct, c + tb * d); ld(xt, x + tb * n); ld(ut, u + tb * m);
       ld(gxx, dl_dx + tb * n); ld(gu, dl_du + tb * m);
+#endif
       if (t == T - 1) {
 #pragma unroll
         for (int i = 0; i < d; ++i) { cdiag[i] = Ct[i][i]; cvec[i] = ct[i]; }
@@ -191,7 +243,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
 #pragma unroll
       for (int i = 0; i < d; ++i)
 #pragma unroll
-        for (int j = 0; j < d; ++j) Cp[i][j] = Ct[i][j] + Mt[j][i];
+        for (int j = 0; j < d; ++j) Cp[i][j] = DZ::hess_nz(j, i) ? Ct[i][j] + Mt[j][i] : Ct[i][j];
 #pragma unroll
       for (int i = 0; i < n; ++i) cb[i] = -gxx[i];
 #pragma unroll
@@ -200,8 +252,8 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
 #pragma unroll
       for (int a = 0; a < m; ++a) { zI[a] = active(tb, a, ut[a]) ? 1.f : 0.f; lb[a] = ub[a] = 0.f; }
       float Kt[m][n], kt[m];
-      if (bd.mode != DILQR_BOUNDS_NONE) rs.template step<GAIN_ZERO_I>(Cp, cb, D, zI, lb, ub, Kt, kt);
-      else rs.template step<GAIN_UNC>(Cp, cb, D, zI, lb, ub, Kt, kt);
+      if (bd.mode != DILQR_BOUNDS_NONE) rs.template step<GAIN_ZERO_I, FS>(Cp, cb, D, zI, lb, ub, Kt, kt);
+      else rs.template step<GAIN_UNC, FS>(Cp, cb, D, zI, lb, ub, Kt, kt);
       float gr[G];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
@@ -213,7 +265,7 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       float cx[n];
 #pragma unroll
       for (int i = 0; i < n; ++i) cx[i] = ct[i];
-      costate_step<n, m>(Ct, cx, xt, ut, D, lam);
+      costate_step<n, m, FS>(Ct, cx, xt, ut, D, lam);
     }
   }
   const bool c_regs = c_offd == 0u && c_dif == 0u, cv_regs = cv_dif == 0u;
@@ -223,11 +275,35 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     float yx[n];
 #pragma unroll
     for (int i = 0; i < n; ++i) yx[i] = 0.f;
+#if DILQR_IMPL_PFC
+    struct CIn {
+      float x[n], u[m], g[G];
+    };
+    auto load_c = [&](int t, CIn& in) {
+      const size_t tb = (size_t)t * B + b;
+      ld(in.x, x + tb * n); ld(in.u, u + tb * m);
+      SoaRec<G>::load(in.g, wsG, T, t, B, b);
+    };
+    CIn cpre;
+    load_c(0, cpre);
+#endif
     for (int t = 0; t < ((DILQR_IMPL_SKIP & 1) ? 0 : T); ++t) {
       size_t tb = (size_t)t * B + b;
       float xt[n], ut[m], gr[G];
+#if DILQR_IMPL_PFC
+      CIn cnx;
+      load_c(t + 1 < T ? t + 1 : t, cnx);
+#pragma unroll
+      for (int i = 0; i < n; ++i) xt[i] = cpre.x[i];
+#pragma unroll
+      for (int a = 0; a < m; ++a) ut[a] = cpre.u[a];
+#pragma unroll
+      for (int i = 0; i < G; ++i) gr[i] = cpre.g[i];
+      cpre = cnx;
+#else
       ld(xt, x + tb * n); ld(ut, u + tb * m);
       SoaRec<G>::load(gr, wsG, T, t, B, b);
+#endif
       float y[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) y[i] = yx[i];
@@ -246,7 +322,8 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         for (int i = 0; i < n; ++i) {
           float s_ = 0.f;
 #pragma unroll
-          for (int j = 0; j < d; ++j) s_ += D[i][j] * y[j];
+          for (int j = 0; j < d; ++j)
+            if (FS::nz(i, j)) s_ += D[i][j] * y[j];
           yx[i] = s_;
         }
       }
@@ -261,9 +338,31 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
     for (int a = 0; a < m; ++a) au[a] = 0.f;
 #pragma unroll
     for (int k = 0; k < p; ++k) dth[k] = 0.f;
+#if DILQR_IMPL_PFD
+    // step t-1's per-step inputs are loaded while step t computes (one wave per
+    // SIMD: nothing else covers the loads' latency); the index clamps at 0, so
+    // the load is unconditional (a conditional one drains the queue at its merge).
+    // Config 4: 0.227 -> 0.221 ms (profiles/r06/ab_implicit_cartpole_prefetch.txt)
+    struct DIn {
+      float x[n], u[m], gx[n], gu[m], y[d], K[m][n];
+    };
+    auto load_in = [&](int t, DIn& in) {
+      const size_t tb = (size_t)t * B + b;
+      ld(in.x, x + tb * n); ld(in.u, u + tb * m);
+      ld(in.gx, dl_dx + tb * n); ld(in.gu, dl_du + tb * m);
+      SoaRec<d>::load(in.y, wsY, T, t, B, b);
+      ld2(in.K, K + ((size_t)(T - 1 - t) * B + b) * m * n);
+    };
+    DIn cin;
+    load_in(T - 1, cin);
+#endif
     for (int t = (DILQR_IMPL_SKIP & 2) ? -1 : T - 1; t >= 0; --t) {
       size_t tb = (size_t)t * B + b;
       float Ct[d][d], ct[d], xt[n], ut[m], gxx[n], gu[m], y[d];
+#if DILQR_IMPL_PFD
+      DIn nin;
+      load_in(t > 0 ? t - 1 : 0, nin);
+#endif
       if (c_regs) {
 #pragma unroll
         for (int i = 0; i < d; ++i)
@@ -278,9 +377,18 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       } else {
         ld(ct, c + tb * d);
       }
+#if DILQR_IMPL_PFD
+#pragma unroll
+      for (int i = 0; i < n; ++i) { xt[i] = cin.x[i]; gxx[i] = cin.gx[i]; }
+#pragma unroll
+      for (int a = 0; a < m; ++a) { ut[a] = cin.u[a]; gu[a] = cin.gu[a]; }
+#pragma unroll
+      for (int i = 0; i < d; ++i) y[i] = cin.y[i];
+#else
       ld(xt, x + tb * n); ld(ut, u + tb * m);
       ld(gxx, dl_dx + tb * n); ld(gu, dl_du + tb * m);
       SoaRec<d>::load(y, wsY, T, t, B, b);
+#endif
       float tau[d];
 #pragma unroll
       for (int i = 0; i < n; ++i) tau[i] = xt[i];
@@ -304,7 +412,14 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
       // Krev = K[t] of the reversed stack = K_{T-1-t}: the gain grad_input pairs with step t+1
       if (t < T - 1) {
         float Kq[m][n], Mt[d][d], Mp[d][p];
+#if DILQR_IMPL_PFD
+#pragma unroll
+        for (int a = 0; a < m; ++a)
+#pragma unroll
+          for (int j = 0; j < n; ++j) Kq[a][j] = cin.K[a][j];
+#else
         ld2(Kq, K + ((size_t)(T - 1 - t) * B + b) * m * n);
+#endif
 #if DILQR_IMPL_SKIP & 4
 #pragma unroll
         for (int i = 0; i < d; ++i)
@@ -326,7 +441,8 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         for (int k = 0; k < n; ++k) {
           float s = 0.f;
 #pragma unroll
-          for (int j = 0; j < d; ++j) s += Mt[j][k] * y[j];
+          for (int j = 0; j < d; ++j)
+            if (DZ::hess_nz(j, k)) s += Mt[j][k] * y[j];
           wx[k] = gxx[k] - s;
         }
         // dtheta_t = -(y^T Mp) + h_t^T gradx_t - dlam_{t+1}^T gradx_{t+1} with
@@ -335,7 +451,8 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         for (int k = 0; k < p; ++k) {
           float s = 0.f;
 #pragma unroll
-          for (int j = 0; j < d; ++j) s += y[j] * Mp[j][k];
+          for (int j = 0; j < d; ++j)
+            if (DZ::dparam_nz(j, k)) s += y[j] * Mp[j][k];
           dth[k] -= s;
         }
 #pragma unroll
@@ -343,17 +460,21 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
           float s = 0.f, s2 = 0.f;
 #pragma unroll
           for (int j = 0; j < d; ++j) {
-            float ml = Mt[j][l];
+            bool any = DZ::hess_nz(j, l);
+            float ml = any ? Mt[j][l] : 0.f;
 #pragma unroll
-            for (int a = 0; a < m; ++a) ml += Mt[j][n + a] * Kq[a][l];
-            s += y[j] * ml;
+            for (int a = 0; a < m; ++a)
+              if (DZ::hess_nz(j, n + a)) { ml += Mt[j][n + a] * Kq[a][l]; any = true; }
+            if (any) s += y[j] * ml;
           }
 #pragma unroll
           for (int i = 0; i < n; ++i) {
-            float dl = D[i][l];
+            bool any = FS::nz(i, l);
+            float dl = any ? D[i][l] : 0.f;
 #pragma unroll
-            for (int a = 0; a < m; ++a) dl += D[i][n + a] * Kq[a][l];
-            s2 += dlam[i] * dl;
+            for (int a = 0; a < m; ++a)
+              if (FS::nz(i, n + a)) { dl += D[i][n + a] * Kq[a][l]; any = true; }
+            if (any) s2 += dlam[i] * dl;
           }
           hx[l] = s2 - s;
         }
@@ -393,12 +514,13 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
 #pragma unroll
           for (int a = 0; a < m; ++a) s2 += Ct[i][n + a] * y[n + a];
 #pragma unroll
-          for (int l = 0; l < n; ++l) s3 += Dl[l][i] * dlam[l];
+          for (int l = 0; l < n; ++l)
+            if (FS::nz(l, i)) s3 += Dl[l][i] * dlam[l];
           nd[i] = ((s + s2) - wx[i]) + s3;
         }
 #pragma unroll
         for (int i = 0; i < n; ++i) dlam[i] = nd[i];
-        costate_step<n, m>(Ct, cx, xt, ut, Dl, lam);
+        costate_step<n, m, FS>(Ct, cx, xt, ut, Dl, lam);
       }
       if (t >= 1) {
         // mu_t = h_t - dlam_t (+ the carry, folded into h_t above); dtheta += f_theta,t^T mu_t
@@ -417,7 +539,8 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
         for (int k = 0; k < p; ++k) {
           float s = 0.f;
 #pragma unroll
-          for (int i = 0; i < n; ++i) s += ft[i][k] * mu[i];
+          for (int i = 0; i < n; ++i)
+            if (DZ::ftheta_nz(i, k)) s += ft[i][k] * mu[i];
           dth[k] += s;
         }
         // the next step's carry: (D_x,t)^T mu_t (the x_grad_xtm1 quirk: no D[0][0]) and (D_u,t)^T mu_t
@@ -426,17 +549,21 @@ __global__ void __launch_bounds__(kBlock) k_implicit_backward(
           float s = 0.f;
 #pragma unroll
           for (int i = 0; i < n; ++i)
-            if (!(D2Of<Model>::XX00_ZERO && i == 0 && l == 0)) s += D[i][l] * mu[i];
+            if (FS::nz(i, l) && !(D2Of<Model>::XX00_ZERO && i == 0 && l == 0)) s += D[i][l] * mu[i];
           ax[l] = s;
         }
 #pragma unroll
         for (int a = 0; a < m; ++a) {
           float s = 0.f;
 #pragma unroll
-          for (int i = 0; i < n; ++i) s += D[i][n + a] * mu[i];
+          for (int i = 0; i < n; ++i)
+            if (FS::nz(i, n + a)) s += D[i][n + a] * mu[i];
           au[a] = s;
         }
       }
+#if DILQR_IMPL_PFD
+      cin = nin;
+#endif
     }
     if (valid) st(dtheta + (size_t)b * p, dth);
   }

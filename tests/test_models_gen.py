@@ -18,6 +18,16 @@ CSRC = os.path.join(ROOT, "differentiable-ilqr_amd", "csrc")
 
 SHIM = r"""
 #include "dilqr_models_gen.h"
+#include "dilqr_d2_sparsity.h"
+#define WRAPZ(MODEL, Dd, N, P)                                                                 \
+extern "C" void MODEL##_nz_tables(int* hess, int* dparam, int* ftheta) {                       \
+  using Z = dilqr::gen::MODEL##D2Z;                                                            \
+  for (int i = 0; i < Dd; ++i) for (int j = 0; j < Dd; ++j) hess[i * Dd + j] = Z::hess_nz(i, j); \
+  for (int i = 0; i < Dd; ++i) for (int k = 0; k < P; ++k) dparam[i * P + k] = Z::dparam_nz(i, k); \
+  for (int i = 0; i < N; ++i) for (int k = 0; k < P; ++k) ftheta[i * P + k] = Z::ftheta_nz(i, k); \
+}
+WRAPZ(Pendulum, 4, 3, 3)
+WRAPZ(Cartpole, 6, 5, 4)
 #define WRAP(MODEL, Dd, N, M, P)                                                              \
 extern "C" void MODEL##_lag_hess(const float* th, const float* x, const float* u,             \
                                  const float* lam, float* out) {                             \
@@ -199,6 +209,35 @@ def test_generated_get_matrices_vs_reference(shim, golden, name):
         for got, key in ((Dp, "D_params"), (Dx, "D_x"), (Du, "D_u"), (xth, "x_theta"), (xx, "x_xtm1")):
             ref = g[f"{name}_gm_{key}"][b]
             assert np.abs(got - ref).max() / scale(ref) < 2e-4, (name, key, b, np.abs(got - ref).max())
+
+
+@pytest.mark.parametrize("name,cls", [("Pendulum", om.Pendulum), ("Cartpole", om.Cartpole)])
+def test_structural_zero_tables(shim, golden, name, cls):
+    """dilqr_d2_sparsity.h's tables (the implicit backward skips those products
+    at compile time) mark exactly the entries the generated lag_hess,
+    lag_dparam and f_theta_cs leave at zero for every input: a declared zero is
+    0.0 at all 64 golden states (with random costates), a declared nonzero is
+    nonzero at some."""
+    g = golden("models_f64")
+    key = name.lower()
+    n, m, p = cls.n_state, cls.n_ctrl, cls.n_params
+    d = n + m
+    tabs = [np.zeros(k, np.int32) for k in (d * d, d * p, n * p)]
+    getattr(shim, f"{name}_nz_tables")(*[t.ctypes.data_as(ctypes.c_void_p) for t in tabs])
+    th = np.array(cls.default_params, np.float32)
+    rng = np.random.RandomState(3)
+    seen = [np.zeros(t.size, bool) for t in tabs]
+    for b in range(g[f"{key}_x"].shape[0]):
+        x32, u32 = g[f"{key}_x"][b].astype(np.float32), g[f"{key}_u"][b].astype(np.float32)
+        l32 = rng.normal(size=n).astype(np.float32)
+        outs = (call(shim, f"{name}_lag_hess", th, x32, u32, l32, out_size=d * d),
+                call(shim, f"{name}_lag_dparam", th, x32, u32, l32, out_size=d * p),
+                call(shim, f"{name}_f_theta_cs", th, x32, u32, out_size=n * p))
+        for k, (o, t) in enumerate(zip(outs, tabs)):
+            assert np.all(o[t == 0] == 0.0), (name, k, np.flatnonzero((t == 0) & (o != 0)))
+            seen[k] |= o != 0
+    for k, t in enumerate(tabs):
+        assert np.all(seen[k][t == 1]), (name, k, np.flatnonzero((t == 1) & ~seen[k]))
 
 
 @pytest.mark.gpu
