@@ -25,6 +25,12 @@
 
 namespace dilqr {
 
+// DILQR_G8_SKIP: timing-only builds (never the shipped library) that replace
+// the per-problem work every lane of a group repeats with stand-ins: bit 0 the
+// Jacobian, bit 1 the 3 x 3 gain solve (VERDICT r05 item 3's pricing)
+#ifndef DILQR_G8_SKIP
+#define DILQR_G8_SKIP 0
+#endif
 constexpr int kG8 = 8;            // lanes per problem
 constexpr int kG8PW = 64 / kG8;   // problems per wave (= per workgroup)
 // Group8Lds's W/Q union relies on a workgroup being exactly one wave64 (LDS
@@ -203,7 +209,16 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
       qb = cbb + 0.f;
     } else {
       float F[n][d];
+#if DILQR_G8_SKIP & 1
+      // timing-only build: a stand-in for the Jacobian (one product per
+      // structural nonzero) to price the per-problem Jacobian every lane repeats
+#pragma unroll
+      for (int k = 0; k < n; ++k)
+#pragma unroll
+        for (int j = 0; j < d; ++j) F[k][j] = FS::nz(k, j) ? xt[(k + j) % n] * 0.001f : 0.f;
+#else
       md.jacobian(xt, ut, F);
+#endif
       {                                            // rows ra, rb of V^T F (row n: v^T F)
         float Wa[d], Wb[d];
 #pragma unroll
@@ -267,7 +282,17 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
       }
     }
     float cola[m], colb[m];
+#if DILQR_G8_SKIP & 2
+    // timing-only build: a diagonal stand-in for the 3x3 gain solve every lane repeats
+#pragma unroll
+    for (int a = 0; a < m; ++a) {
+      const float ir = __builtin_amdgcn_rcpf(Quu[a][a]);
+      cola[a] = -rha[a] * ir;
+      colb[a] = -rhb[a] * ir;
+    }
+#else
     group_gains_col2<n, m, MODE>(ja, jb, Quu, rha, rhb, qu, lo, hi, cola, colb, prev_k, have_prev);
+#endif
     // V_t columns ra, rb (row n's lane: v_t), group_riccati_step_t's expressions
     float Kall[m][n];
     if constexpr (!SCHUR) {

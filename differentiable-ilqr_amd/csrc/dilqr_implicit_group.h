@@ -192,7 +192,8 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
   const bool crow_regs = c_offd == 0u && c_dif == 0u, cv_regs = cv_dif == 0u;
   // ---------------- C (t up): the rollout y of the modified problem (linear, alpha = 1)
   // (DILQR_IMPL_SKIP: timing-only builds that leave out pass C (bit 1) or pass D
-  // (bit 2) to split the kernel's time by pass; never the shipped library)
+  // (bit 2) to split the kernel's time by pass, or in pass D the dC/dc stores
+  // (4), mcol + mp_row (8), xth_row + xx_row (16); never the shipped library)
   {
     float yx = 0.f;                                        // lane r < n: y_t[r]
     // DILQR_IMPL_C_PF: step t+1's inputs (x, u, this lane's gain column, k)
@@ -282,7 +283,12 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
 #pragma unroll
       for (int j = 0; j < d; ++j) { yr = (j == r) ? y[j] : yr; taur = (j == r) ? tau[j] : taur; }
       // dC_t row r = -0.5 (y_r tau^T + tau_r y^T), dc_t = -y   (lqr_step_explicit.py:296-303)
-      if (valid && r < d) {
+      // (Round 6: these rows staged through LDS and stored as the wave's
+      // contiguous 4-KiB run, 64 contiguous 16-byte chunks per instruction:
+      // 1.375 -> 1.386 ms, no gain — the stores' cost is the 1 GB of dC itself
+      // at the write rate, 0.17 ms (DILQR_IMPL_SKIP & 4),
+      // profiles/r06/ab_implicit_rocket_split.txt)
+      if (valid && r < d && !(DILQR_IMPL_SKIP & 4)) {
         float dCr[d];
 #pragma unroll
         for (int j = 0; j < d; ++j) dCr[j] = -0.5f * (yr * tau[j] + taur * y[j]);
@@ -304,8 +310,15 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
           float lam1[n];
 #pragma unroll
           for (int i = 0; i < n; ++i) lam1[i] = I.lam[i];  // lam_{t+1}
+#if DILQR_IMPL_SKIP & 8
+#pragma unroll
+          for (int j = 0; j < d; ++j) Mc[j] = 0.f * lam1[j % n];
+#pragma unroll
+          for (int k = 0; k < p; ++k) Mp[k] = 0.f * lam1[k];
+#else
           D2::mcol(r, theta, ith, xt, ut, lam1, Mc);
           D2::mp_row(r, theta, ith, xt, ut, lam1, Mp);
+#endif
         }
         __syncthreads();
         float z = 0.f;                                     // (M_t^T y_t)[r]
@@ -366,10 +379,19 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
         if (r < n) {
           mu = hx - nd;
           float ft[p];
+#if DILQR_IMPL_SKIP & 16
+#pragma unroll
+          for (int k = 0; k < p; ++k) ft[k] = 0.f * xt[k];
+#pragma unroll
+          for (int l = 0; l < n; ++l) axr[l] = 0.f * xt[l];
+#else
           D2::xth_row(r, theta, ith, xt, ut, ft);
+#endif
 #pragma unroll
           for (int k = 0; k < p; ++k) acc[k] += ft[k] * mu;
+#if !(DILQR_IMPL_SKIP & 16)
           D2::xx_row(r, theta, ith, xt, ut, axr);
+#endif
         }
 #pragma unroll
         for (int a = 0; a < m; ++a) au[a] = group_sum(r < n ? L.F[r][n + a] * mu : 0.f);
