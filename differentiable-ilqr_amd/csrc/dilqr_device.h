@@ -528,6 +528,25 @@ struct DenseF {
   static constexpr bool nz(int, int) { return true; }
 };
 
+// A sum of products whose first term starts it (s = a*b, then s += a*b): no
+// leading "0 +" — which the compiler must keep (0 + -0 is +0) and which costs
+// an instruction wherever the first factor is a literal 1 the product folds
+// away (a Jacobian's identity entries).  The values equal the 0-started sum's
+// except for the sign of an exact zero.  Under full unrolling `first` is a
+// compile-time constant.
+#ifndef DILQR_ACC0
+#define DILQR_ACC0 0                        // 1: the 0-started sums (A/B builds)
+#endif
+struct Acc {
+  float s = 0.f;
+  bool first = true;
+  DEV void add(float a, float b) {
+    if (first && !DILQR_ACC0) s = a * b;
+    else s += a * b;
+    first = false;
+  }
+};
+
 template <int D>
 DEV bool bitwise_symmetric(const float (&C)[D][D]) {
   unsigned asym = 0u;                       // an xor/or reduction, one compare
@@ -582,20 +601,21 @@ struct RiccatiState {
       for (int l = 0; l < N; ++l)
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-          float s = 0.f;
+          Acc s;
 #pragma unroll
           for (int kk = 0; kk < N; ++kk)
-            if (FS::nz(kk, j)) s += V[l][kk] * F[kk][j];
-          W[l][j] = s;
+            if (FS::nz(kk, j)) s.add(V[l][kk], F[kk][j]);
+          W[l][j] = s.s;
         }
 #pragma unroll
       for (int i = 0; i < D; ++i)
 #pragma unroll
         for (int j = i; j < D; ++j) {
-          float s = 0.f;
+          Acc a;
 #pragma unroll
           for (int l = 0; l < N; ++l)
-            if (FS::nz(l, i)) s += F[l][i] * W[l][j];
+            if (FS::nz(l, i)) a.add(F[l][i], W[l][j]);
+          const float s = a.s;
           Q[i][j] = (DIAG && i != j) ? s : C[i][j] + s;     // DIAG: C[i][j] is +0.0
           if (j != i) Q[j][i] = (DIAG) ? s : C[j][i] + s;
         }
@@ -606,31 +626,32 @@ struct RiccatiState {
       for (int i = 0; i < D; ++i)
 #pragma unroll
         for (int kk = 0; kk < N; ++kk) {
-          float s = 0.f;
+          Acc s;
 #pragma unroll
           for (int l = 0; l < N; ++l)
-            if (FS::nz(l, i)) s += F[l][i] * V[l][kk];
-          P[i][kk] = s;
+            if (FS::nz(l, i)) s.add(F[l][i], V[l][kk]);
+          P[i][kk] = s.s;
         }
 #pragma unroll
       for (int i = 0; i < D; ++i)
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-          float s = 0.f;
+          Acc a;
 #pragma unroll
           for (int kk = 0; kk < N; ++kk)
-            if (FS::nz(kk, j)) s += P[i][kk] * F[kk][j];
+            if (FS::nz(kk, j)) a.add(P[i][kk], F[kk][j]);
+          const float s = a.s;
           Q[i][j] = (DIAG && i != j) ? s : C[i][j] + s;     // DIAG: C[i][j] is +0.0
         }
     }
     // q = cb + F^T v
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      float s = 0.f;
+      Acc s;
 #pragma unroll
       for (int l = 0; l < N; ++l)
-        if (FS::nz(l, i)) s += F[l][i] * v[l];
-      q[i] = cb[i] + s;
+        if (FS::nz(l, i)) s.add(F[l][i], v[l]);
+      q[i] = cb[i] + s.s;
     }
     // partitions (lqr_step_explicit.py:78-83)
     float Quu[M][M], qu[M];
