@@ -2,6 +2,9 @@
 stream.  Every function here is one (or a few) libdilqr.so calls; nothing
 computes on the host.
 """
+import collections
+import os
+
 import torch
 
 from . import _native as N
@@ -342,6 +345,14 @@ class MPCSolve:
         N.call("dilqr_mpc_finish_fixed_f32", self.T, self.m, self.B, int(iterations), self.state,
                N.stream(self.Xs.device))
 
+    def poll_buffer(self, i):
+        """Pinned host buffer i (a small ring) for mpc_solve's non-blocking stop
+        polls; a buffer is reused only after its poll was read."""
+        if not hasattr(self, "_polls"):
+            self._polls = [torch.empty(N.CTRL_INTS, dtype=torch.int32, pin_memory=True)
+                           for _ in range(POLL_AHEAD + 2)]
+        return self._polls[i % len(self._polls)]
+
     def _ctrl_now(self):
         k = max(self.last_iteration, 0)
         return self.ctrl.view(2, N.CTRL_INTS)[k & 1]        # solve_small writes both words
@@ -370,6 +381,11 @@ class MPCSolve:
             return int(ctrl[0].item())
         return self.last_iteration + 1
 
+
+# runs of the stop-rule loop queued behind the oldest unread stop-flag copy
+# (mpc_solve): the host waits for a poll only this far behind the device
+# (DILQR_POLL_AHEAD=0: a blocking poll after every run, the round-5 loop)
+POLL_AHEAD = int(os.environ.get("DILQR_POLL_AHEAD", "2"))
 
 # dilqr_mpc_solve_small_f32: batches one workgroup holds, thread-per-problem models
 SMALL_BATCH_MAX = 256
@@ -421,13 +437,36 @@ def mpc_solve(model_id, theta, x_init, C, c, T, u_init=None, u_lower=None, u_upp
         x, u = sv.gather_best()
         return x, u, sv.best_cost, sv.best_du, sv
     sv.begin(model_id, theta, x_init, u_init)
-    # runs of check_every iterations per library call, the stop flag polled
-    # between runs (iterations after a stop are device no-ops)
+    # runs of check_every iterations per library call (iterations after a stop
+    # are device no-ops).  The stop flag is polled without stalling the device:
+    # after each run the control word is copied to pinned host memory behind an
+    # event, and the host only waits for the copy of a run once POLL_AHEAD runs
+    # are queued behind it — so the GPU never drains while the host looks (a
+    # blocking poll every 8 iterations idled it once per poll), and at most
+    # POLL_AHEAD runs of no-op launches follow a stop.
     step = check_every if check_every else max(lqr_iter, 1)
+    polls = collections.deque()
+    n_polls = 0
+    stream = torch.cuda.current_stream(x_init.device)
     for i0 in range(0, lqr_iter, step):
         sv.iterate_range(model_id, theta, x_init, C, c, bounds, linesearch_decay, max_linesearch_iter, i0,
                          min(step, lqr_iter - i0), best_cost_eps, eps, not_improved_lim)
-        if i0 + step < lqr_iter and sv.stopped:
+        if i0 + step >= lqr_iter:
+            break
+        host = sv.poll_buffer(n_polls)            # a ring longer than the polls in flight
+        n_polls += 1
+        host.copy_(sv._ctrl_now(), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        polls.append((ev, host))
+        stopped = False
+        while polls and (len(polls) > POLL_AHEAD or polls[0][0].query()):
+            ev0, host0 = polls.popleft()
+            ev0.synchronize()
+            if int(host0[1]):
+                stopped = True
+                break
+        if stopped:
             break
     del keep
     x, u = sv.gather_best()
