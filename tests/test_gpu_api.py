@@ -310,3 +310,51 @@ def test_small_batch_solve_edges(B, T, iters, mls):
     for f in ("best_cost", "best_du", "full_du_norm", "cost", "alpha"):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
     del keep
+
+
+@pytest.mark.parametrize("eps,lim,iters", [(5e-2, 5, 60), (1e-4, 5, 40), (0.0, 2, 40)])
+def test_pipelined_stop_polls_equal_blocking_polls(eps, lim, iters):
+    """Above SMALL_BATCH_MAX the stop-rule loop runs per-iteration launches and
+    polls the stop flag through pinned-memory copies behind events, waiting
+    only POLL_AHEAD runs behind the device (round 6).  The result — best
+    trajectories, costs, best_du, the iterations that ran, the stop flag — is
+    the blocking poll's (POLL_AHEAD = 0) and the plain per-iteration loop's
+    (iterations after a stop are device no-ops), stopped early or not."""
+    from dilqr import _native as N
+    from dilqr import ops
+    from dilqr.env_dx.cartpole import CartpoleDx
+    B, T = 512, 25
+    dx = CartpoleDx()
+    rng = np.random.RandomState(12)
+    th = rng.uniform(-np.pi, np.pi, B)
+    x0 = torch.tensor(np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                                rng.uniform(-1, 1, B)], 1), dtype=torch.float32, device=DEV)
+    q, p = dx.get_true_obj()
+    C = torch.diag(q).repeat(T, B, 1, 1).to(DEV).contiguous()
+    c = p.repeat(T, B, 1).to(DEV).contiguous()
+    th_ = ops.theta_of(dx, x0)
+    assert B > ops.SMALL_BATCH_MAX
+    out = {}
+    keep = ops.POLL_AHEAD
+    try:
+        for pa in (2, 0):
+            ops.POLL_AHEAD = pa
+            x, u, cost, du, sv = ops.mpc_solve(dx.model_id, th_, x0, C, c, T, u_lower=-10.0, u_upper=10.0,
+                                               lqr_iter=iters, eps=eps, linesearch_decay=0.5, max_linesearch_iter=2,
+                                               not_improved_lim=lim)
+            out[pa] = (x, u, cost, du, sv.iterations, sv.stopped)
+    finally:
+        ops.POLL_AHEAD = keep
+    nb, kb = N.make_bounds(-10.0, 10.0)
+    ref = ops.MPCSolve(T, B, 5, 1, DEV)
+    ref.begin(dx.model_id, th_, x0)
+    for i in range(iters):
+        ref.iterate(dx.model_id, th_, x0, C, c, nb, 0.5, 2, i, 1e-4, eps, lim)
+    xr, ur = ref.gather_best()
+    print(f"\neps {eps} lim {lim}: ran {out[2][4]} of {iters} (stopped {out[2][5]}), reference loop {ref.iterations}")
+    for pa in (2, 0):
+        x, u, cost, du, its, stopped = out[pa]
+        assert torch.equal(x, xr) and torch.equal(u, ur), pa
+        assert torch.equal(cost, ref.best_cost) and torch.equal(du, ref.best_du), pa
+        assert its == ref.iterations and stopped == ref.stopped, (pa, its, ref.iterations)
+    del kb
