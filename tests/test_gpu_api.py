@@ -312,8 +312,11 @@ def test_small_batch_solve_edges(B, T, iters, mls):
     del keep
 
 
-@pytest.mark.parametrize("eps,lim,iters", [(5e-2, 5, 60), (1e-4, 5, 40), (0.0, 2, 40)])
-def test_pipelined_stop_polls_equal_blocking_polls(eps, lim, iters):
+@pytest.mark.parametrize("model,bounds,eps,lim,iters", [("pendulum", (-2.0, 2.0), 1e-3, 5, 60),
+                                                      ("cartpole", None, 5e-2, 5, 60),
+                                                      ("cartpole", (-10.0, 10.0), 1e-4, 5, 40),
+                                                      ("cartpole", (-10.0, 10.0), 0.0, 2, 40)])
+def test_pipelined_stop_polls_equal_blocking_polls(model, bounds, eps, lim, iters):
     """Above SMALL_BATCH_MAX the stop-rule loop runs per-iteration launches and
     polls the stop flag through pinned-memory copies behind events, waiting
     only POLL_AHEAD runs behind the device (round 6).  The result — best
@@ -323,12 +326,21 @@ def test_pipelined_stop_polls_equal_blocking_polls(eps, lim, iters):
     from dilqr import _native as N
     from dilqr import ops
     from dilqr.env_dx.cartpole import CartpoleDx
-    B, T = 512, 25
-    dx = CartpoleDx()
+    from dilqr.env_dx.pendulum import PendulumDx
+    B = 512
     rng = np.random.RandomState(12)
-    th = rng.uniform(-np.pi, np.pi, B)
-    x0 = torch.tensor(np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
-                                rng.uniform(-1, 1, B)], 1), dtype=torch.float32, device=DEV)
+    if model == "cartpole":
+        T, dx, decay, mls = 25, CartpoleDx(), 0.5, 2
+        th = rng.uniform(-np.pi, np.pi, B)
+        x0 = np.stack([rng.uniform(-.5, .5, B), rng.uniform(-.5, .5, B), np.cos(th), np.sin(th),
+                       rng.uniform(-1, 1, B)], 1)
+    else:
+        T, dx, decay, mls = 20, PendulumDx(), 0.2, 5
+        th = rng.uniform(-np.pi / 2, np.pi / 2, B)
+        x0 = np.stack([np.cos(th), np.sin(th), rng.uniform(-1, 1, B)], 1)
+    x0 = torch.tensor(x0, dtype=torch.float32, device=DEV)
+    n, m = dx.n_state, dx.n_ctrl
+    lo, hi = bounds if bounds else (None, None)
     q, p = dx.get_true_obj()
     C = torch.diag(q).repeat(T, B, 1, 1).to(DEV).contiguous()
     c = p.repeat(T, B, 1).to(DEV).contiguous()
@@ -339,19 +351,22 @@ def test_pipelined_stop_polls_equal_blocking_polls(eps, lim, iters):
     try:
         for pa in (2, 0):
             ops.POLL_AHEAD = pa
-            x, u, cost, du, sv = ops.mpc_solve(dx.model_id, th_, x0, C, c, T, u_lower=-10.0, u_upper=10.0,
-                                               lqr_iter=iters, eps=eps, linesearch_decay=0.5, max_linesearch_iter=2,
-                                               not_improved_lim=lim)
+            x, u, cost, du, sv = ops.mpc_solve(dx.model_id, th_, x0, C, c, T, u_lower=lo, u_upper=hi,
+                                               lqr_iter=iters, eps=eps, linesearch_decay=decay,
+                                               max_linesearch_iter=mls, not_improved_lim=lim)
             out[pa] = (x, u, cost, du, sv.iterations, sv.stopped)
     finally:
         ops.POLL_AHEAD = keep
-    nb, kb = N.make_bounds(-10.0, 10.0)
-    ref = ops.MPCSolve(T, B, 5, 1, DEV)
+    nb, kb = N.make_bounds(lo, hi)
+    ref = ops.MPCSolve(T, B, n, m, DEV)
     ref.begin(dx.model_id, th_, x0)
     for i in range(iters):
-        ref.iterate(dx.model_id, th_, x0, C, c, nb, 0.5, 2, i, 1e-4, eps, lim)
+        ref.iterate(dx.model_id, th_, x0, C, c, nb, decay, mls, i, 1e-4, eps, lim)
     xr, ur = ref.gather_best()
-    print(f"\neps {eps} lim {lim}: ran {out[2][4]} of {iters} (stopped {out[2][5]}), reference loop {ref.iterations}")
+    print(f"\n{model} {bounds} eps {eps} lim {lim}: ran {out[2][4]} of {iters} (stopped {out[2][5]}), "
+          f"reference loop {ref.iterations}")
+    if model == "pendulum":
+        assert out[2][5], "this case is meant to stop early"
     for pa in (2, 0):
         x, u, cost, du, its, stopped = out[pa]
         assert torch.equal(x, xr) and torch.equal(u, ur), pa
