@@ -49,8 +49,25 @@ struct ImplicitGroupLds {
   float dlam[kG];                              // dlam_{t+1} (D)
 };
 
-template <class Model, class D2, int MODE>
-__global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_group(
+// PASSES: which of the passes this launch runs (1 = B, 2 = C, 4 = D; 7 = all in
+// one launch).  Split launches run the same code per pass; what pass B hands
+// pass D in registers when they share a launch — whether each lane's cost row
+// and c_t entry are the same diagonal row for all t (crow_regs, cv_regs) and
+// their values — is kept as one flag word per problem in a spare word of the
+// t = 0 workspace record (KG column 14: no gain lives there, pass C never reads
+// it) and re-read from C's step T-1 row in pass D.  A pass alone needs fewer
+// registers than the three together: 3 waves per SIMD instead of 2 for passes
+// B and C.  Not the default (tu_implicit_rocket.hip DILQR_IMPL_SPLIT: no gain).
+#ifndef DILQR_IMPL_SPLIT_WAVES
+#define DILQR_IMPL_SPLIT_WAVES 3
+#endif
+#ifndef DILQR_IMPL_D_WAVES
+#define DILQR_IMPL_D_WAVES 2                 // at 3 pass D spills (168 VGPRs + 104 B scratch)
+#endif
+template <class Model, class D2, int MODE, int PASSES = 7>
+__global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
+                                      : PASSES == 4 ? DILQR_IMPL_D_WAVES
+                                                    : DILQR_IMPL_SPLIT_WAVES) k_implicit_backward_group(
     int T, int B, const float* __restrict__ theta, const float* __restrict__ C, const float* __restrict__ c,
     const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ K,
     const float* __restrict__ dl_dx, const float* __restrict__ dl_du, Bounds bd, float* __restrict__ ws,
@@ -96,7 +113,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
   float cdg = 0.f, cvr = 0.f;
   unsigned c_offd = 0u, c_dif = 0u, cv_dif = 0u;
   // ---------------- B: costates, M_t, Riccati of the C + M^T problem (active set masked)
-  {
+  if constexpr ((PASSES & 1) != 0) {
     if (r < n) {
 #pragma unroll
       for (int kk = 0; kk < GroupLds<n, m>::W; ++kk) L.V[r][kk] = 0.f;
@@ -189,12 +206,32 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
     }
   }
   // per lane: row r of C and c_t[r] from registers in pass D
-  const bool crow_regs = c_offd == 0u && c_dif == 0u, cv_regs = cv_dif == 0u;
+  bool crow_regs = c_offd == 0u && c_dif == 0u, cv_regs = cv_dif == 0u;
+  constexpr int kFlagSlot = W::KG + 14;            // t = 0 record, gain column 14: unused (r < n = 13 and k at n)
+  static_assert(Model::N + 1 < 15, "the flag word needs a free gain column");
+  if constexpr ((PASSES & 1) != 0 && (PASSES & 4) == 0) {
+    // hand the flags to the pass-D launch: bit r = crow_regs of lane r, bit 16 + r = cv_regs
+    const unsigned long long bc = __ballot(crow_regs), bv = __ballot(cv_regs);
+    const int sh = threadIdx.x & ~(kG - 1);
+    const unsigned word = (unsigned)((bc >> sh) & 0xFFFFull) | ((unsigned)((bv >> sh) & 0xFFFFull) << 16);
+    if (valid && r == 0) rec(0)[kFlagSlot] = __uint_as_float(word);
+  }
+  if constexpr ((PASSES & 4) != 0 && (PASSES & 1) == 0) {
+    const unsigned word = __float_as_uint(rec(0)[kFlagSlot]);
+    crow_regs = (word >> r) & 1u;
+    cv_regs = (word >> (16 + r)) & 1u;
+    // the register row and value pass B kept: step T-1's (equal at every t when the flag is set)
+    if (r < d) {
+      const size_t tb = (size_t)(T - 1) * B + b;
+      if (crow_regs) cdg = C[(tb * d + r) * d + r];
+      if (cv_regs) cvr = c[tb * d + r];
+    }
+  }
   // ---------------- C (t up): the rollout y of the modified problem (linear, alpha = 1)
   // (DILQR_IMPL_SKIP: timing-only builds that leave out pass C (bit 1) or pass D
   // (bit 2) to split the kernel's time by pass, or in pass D the dC/dc stores
   // (4), mcol + mp_row (8), xth_row + xx_row (16); never the shipped library)
-  {
+  if constexpr ((PASSES & 2) != 0) {
     float yx = 0.f;                                        // lane r < n: y_t[r]
     // DILQR_IMPL_C_PF: step t+1's inputs (x, u, this lane's gain column, k)
     // loaded while step t computes — pass C is a short chain per step behind its
@@ -248,7 +285,7 @@ __global__ void __launch_bounds__(64, kGroupWavesPerSimd) k_implicit_backward_gr
     }
   }
   // ---------------- D: lam, w, dlam, dC, dc, dtheta (t down)
-  {
+  if constexpr ((PASSES & 4) != 0) {
     float acc[p];
 #pragma unroll
     for (int k = 0; k < p; ++k) acc[k] = 0.f;
