@@ -2,6 +2,14 @@
 // lqr_step_explicit.py:54-162), one lane or one 16-lane group per problem.
 #include "dilqr_common.h"
 
+// DILQR_GROUP_SWEEP_SMALL (default 0; timing builds only): batches of at most
+// this many cartpole problems take the 16-lane group sweep (dilqr_group.h,
+// lane r owns row r) instead of one lane per problem — the small-batch mapping
+// of DESIGN.md §6, measured in profiles/r06/small_sweep_mapping.txt
+#ifndef DILQR_GROUP_SWEEP_SMALL
+#define DILQR_GROUP_SWEEP_SMALL 0
+#endif
+
 namespace dilqr {
 
 // ============================================================ Riccati sweep
@@ -110,6 +118,22 @@ int dilqr_lqr_backward_f32(int n, int m, int T, int B, const float* C, const flo
   int mode = bounds.mode != DILQR_BOUNDS_NONE ? GAIN_BOX
              : u_zero_I ? GAIN_ZERO_I
              : (m_solver == DILQR_SOLVE_CHOL && m > 1) ? GAIN_CHOL : GAIN_UNC;
+#if DILQR_GROUP_SWEEP_SMALL
+  // timing builds only (tools/small_sweep_mapping.py): cartpole's sweep on the
+  // 16-lane row-per-lane group mapping for small batches, against the lane sweep
+  if (n == 5 && m == 1 && B <= DILQR_GROUP_SWEEP_SMALL) {
+#define GLAUNCH(MODE_)                                                                                       \
+    k_lqr_backward_group<5, 1, MODE_><<<grid_group(B), 64, 0, S(stream)>>>(T, B, C, c, x, u, F, bd, u_zero_I, K, \
+                                                                           k, n_qp_iter, n_qp_step)
+    switch (mode) {
+      case GAIN_UNC: GLAUNCH(GAIN_UNC); break;
+      case GAIN_ZERO_I: GLAUNCH(GAIN_ZERO_I); break;
+      default: GLAUNCH(GAIN_BOX); break;
+    }
+#undef GLAUNCH
+    return launched();
+  }
+#endif
 #define LAUNCH(N_, M_, MODE_) \
   k_lqr_backward<N_, M_, MODE_><<<grid_for(B), kBlock, 0, S(stream)>>>(T, B, C, c, x, u, F, bd, u_zero_I, K, k, n_qp_iter, \
                                                                        n_qp_step)
