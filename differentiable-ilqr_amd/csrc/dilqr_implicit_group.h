@@ -14,7 +14,8 @@
 //   xth_row(r) row r of dx_{t+1}/dtheta
 // and Model::jac_row(r) (row r of D_t, which is also x_grad_utm1's source).
 // Vectors every lane needs in full (lam, dlam, y, the adjoint carry) go through LDS; the
-// Riccati step of the modified problem is group_riccati_step.
+// Riccati step of the modified problem is the sweeps' transposed step
+// (group_riccati_step_c, DILQR_IMPL_BT).
 #pragma once
 
 #include "dilqr_group.h"
@@ -49,6 +50,43 @@ struct ImplicitGroupLds {
   float dlam[kG];                              // dlam_{t+1} (D)
 };
 
+// DILQR_IMPL_BT (default 1): pass B's Riccati step in the sweeps' transposed
+// form (group_riccati_step_c: V_{t+1} column r in lane r's registers, W = V^T F
+// and Q's rows exchanged through LDS, both products over the Jacobian's
+// structural nonzeros, Rocket::FSparsity 69 of 208, read from the F rows the
+// costates need in LDS anyway; the unconstrained value update in Schur form)
+// instead of the rows-of-V step (group_riccati_step: two dense 13x13x16
+// products on V and F rows from LDS).  0 keeps the old step (A/B only).
+#ifndef DILQR_IMPL_BT
+#define DILQR_IMPL_BT 1
+#endif
+// LDS of one problem for the transposed step: W^T and Q share their words (a
+// workgroup is one wave, whose LDS accesses complete in program order: every
+// lane's read of its W column precedes the Q row writes), F rows beside them;
+// padded to 16 words mod 32 so the two problems of a half-wave read disjoint
+// banks (as GroupLdsT)
+template <int n, int m>
+struct ImplicitStepLds {
+  static constexpr int d = n + m;
+  static constexpr int W = 16;
+  static constexpr int QS = W + 4;
+  static constexpr int RS = GroupLds<n, m>::RS;
+  union {
+    float Wt[n + 1][W];
+    float Q[d][QS];
+  };
+  float Kk[m][W];
+  float F[n][RS];
+  static constexpr int kWords = ((n + 1) * W > d * QS ? (n + 1) * W : d * QS) + m * W + n * RS;
+  float pad[((16 - kWords % 32) % 32 + 32) % 32];
+};
+static_assert(sizeof(ImplicitStepLds<13, 3>) / 4 % 32 == 16, "bank offset between groups");
+template <class LdsT>
+struct FRowsLds {
+  const LdsT& L;
+  DEV float at(int k, int j) const { return L.F[k][j]; }
+};
+
 // PASSES: which of the passes this launch runs (1 = B, 2 = C, 4 = D; 7 = all in
 // one launch).  Split launches run the same code per pass; what pass B hands
 // pass D in registers when they share a launch — whether each lane's cost row
@@ -75,14 +113,19 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
   constexpr int n = Model::N, m = Model::M, p = Model::P, d = n + m;
   static_assert(d <= kG, "one row per lane");
   using W = ImplicitGroupWs<Model>;
-  __shared__ GroupLds<n, m> Ls[kGPW];
+#if DILQR_IMPL_BT
+  using LdsB = ImplicitStepLds<n, m>;
+#else
+  using LdsB = GroupLds<n, m>;
+#endif
+  __shared__ LdsB Ls[kGPW];
   __shared__ ImplicitGroupLds<n, p> Is[kGPW];
   const int r = threadIdx.x & (kG - 1);
   const int gp = threadIdx.x / kG;
   const int b0 = blockIdx.x * kGPW + gp;
   const bool valid = b0 < B;
   const int b = valid ? b0 : B - 1;           // a padding group recomputes problem B-1, writes nothing
-  GroupLds<n, m>& L = Ls[gp];
+  LdsB& L = Ls[gp];
   ImplicitGroupLds<n, p>& I = Is[gp];
   Model md;
   md.load(theta);
@@ -114,11 +157,17 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
   unsigned c_offd = 0u, c_dif = 0u, cv_dif = 0u;
   // ---------------- B: costates, M_t, Riccati of the C + M^T problem (active set masked)
   if constexpr ((PASSES & 1) != 0) {
+#if DILQR_IMPL_BT
+    float U[n];                                        // column r of V_{t+1} (lane n: v_{t+1})
+#pragma unroll
+    for (int i = 0; i < n; ++i) U[i] = 0.f;
+#else
     if (r < n) {
 #pragma unroll
       for (int kk = 0; kk < GroupLds<n, m>::W; ++kk) L.V[r][kk] = 0.f;
       L.v[r] = 0.f;
     }
+#endif
     if (r < kG) I.vec[r] = 0.f;
     float prev_k[m];
 #pragma unroll
@@ -151,7 +200,12 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
       for (int i = 0; i < n; ++i) lam1[i] = I.vec[i];     // lam_{t+1} (0 at t = T-1)
       float Mc[d];
       if (t < T - 1) {
+#if DILQR_IMPL_SKIP & 64                                   // timing only: no M_t column in pass B
+#pragma unroll
+        for (int j = 0; j < d; ++j) Mc[j] = 0.f * lam1[j % n];
+#else
         D2::mcol(r, theta, ith, xt, ut, lam1, Mc);
+#endif
         if (r < n) {
           float Fr[d];
           md.jac_row_sel(r, xt, ut, Fr);
@@ -177,7 +231,24 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
         lb[a] = ub[a] = 0.f;
       }
       float Kt[m][n], kt[m];
+#if DILQR_IMPL_SKIP & 32                                   // timing only: no Riccati step (Cp kept live)
+      {
+        float s = -gr;
+#pragma unroll
+        for (int j = 0; j < d; ++j) s += Cp[j];
+        if (r < n) L.Kk[0][r] = s;
+        __syncthreads();
+      }
+#elif DILQR_IMPL_BT
+      // t = T-1 through the general step: F's rows and U are zero there, so W = 0
+      // and Q = Cp + 0, q = -g + 0, the LAST step's values bit for bit
+      float col[m];
+      group_riccati_step_c<n, m, MODE, typename Model::FSparsity, false>(
+          L, r, FRowsLds<LdsB>{L}, U, CostRegs<d>{Cp, -gr}, zI, lb, ub, col, prev_k, have_prev, nqp);
+      (void)Kt; (void)kt;
+#else
       group_riccati_step<n, m, MODE>(L, r, Cp, -gr, zI, lb, ub, Kt, kt, prev_k, have_prev, nqp);
+#endif
       // lam_t = Cxx x + Cxu u + c_x + F_x^T lam_{t+1}   (lqr_step_explicit.py:305-319)
       float lam_r = 0.f;
       if (r < n) {
@@ -192,6 +263,12 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
       }
       if (valid) {
         float* R0 = rec(t);
+#if DILQR_IMPL_BT && !(DILQR_IMPL_SKIP & 32)
+        if (r <= n) {                                      // lane r < n: K[:, r]; lane n: k
+#pragma unroll
+          for (int a = 0; a < m; ++a) R0[W::KG + a * kG + r] = col[a];
+        }
+#else
         if (r < n) {
 #pragma unroll
           for (int a = 0; a < m; ++a) R0[W::KG + a * kG + r] = L.Kk[a][r];
@@ -199,6 +276,7 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
 #pragma unroll
           for (int a = 0; a < m; ++a) R0[W::KG + a * kG + n] = L.Kk[a][GroupLds<n, m>::W];
         }
+#endif
       }
       __syncthreads();                                     // every lane is done with lam_{t+1}, F, Kk
       if (r < n) I.vec[r] = lam_r;
@@ -230,7 +308,8 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
   // ---------------- C (t up): the rollout y of the modified problem (linear, alpha = 1)
   // (DILQR_IMPL_SKIP: timing-only builds that leave out pass C (bit 1) or pass D
   // (bit 2) to split the kernel's time by pass, or in pass D the dC/dc stores
-  // (4), mcol + mp_row (8), xth_row + xx_row (16); never the shipped library)
+  // (4), mcol + mp_row (8), xth_row + xx_row (16); in pass B the Riccati step
+  // (32) or mcol (64); never the shipped library)
   if constexpr ((PASSES & 2) != 0) {
     float yx = 0.f;                                        // lane r < n: y_t[r]
     // DILQR_IMPL_C_PF: step t+1's inputs (x, u, this lane's gain column, k)
