@@ -26,6 +26,15 @@
 #ifndef DILQR_IMPL_C_PF
 #define DILQR_IMPL_C_PF 1
 #endif
+// DILQR_IMPL_GPFB / GPFD: passes B / D loading step t-1's inputs one step
+// ahead (A/B only: 1.16-1.25 ms with either, both or neither, within the
+// noise; profiles/r06/ab_implicit_rocket_prefetch_BD.txt)
+#ifndef DILQR_IMPL_GPFB
+#define DILQR_IMPL_GPFB 0
+#endif
+#ifndef DILQR_IMPL_GPFD
+#define DILQR_IMPL_GPFD 0
+#endif
 
 namespace dilqr {
 
@@ -175,16 +184,44 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
     bool have_prev = false;
     int nqp = 0;
     __syncthreads();
+    // DILQR_IMPL_GPFB: step t-1's inputs (x, u, the cost row, c, the loss
+    // gradient) loaded while step t computes
+    struct BIn {
+      float x[n], u[m], C[d], c, g;
+    };
+    auto load_b = [&](int t, BIn& in) {
+      const size_t tb = (size_t)t * B + b;
+      load_tau(tb, in.x, in.u);
+#pragma unroll
+      for (int j = 0; j < d; ++j) in.C[j] = 0.f;
+      in.c = in.g = 0.f;
+      if (r < d) {
+        ld(in.C, C + (tb * d + r) * d);
+        in.c = c[tb * d + r];
+        in.g = r < n ? dl_dx[tb * n + r] : dl_du[tb * m + (r - n)];
+      }
+    };
+    BIn nx;
+    if (DILQR_IMPL_GPFB) load_b(T - 1, nx);
     for (int t = T - 1; t >= 0; --t) {
       const size_t tb = (size_t)t * B + b;
       float xt[n], ut[m], Crow[d], cr = 0.f, gr = 0.f;
-      load_tau(tb, xt, ut);
+      {
+        BIn cur;
+        if (DILQR_IMPL_GPFB) {
+          cur = nx;
+          if (t > 0) load_b(t - 1, nx);
+        } else {
+          load_b(t, cur);
+        }
 #pragma unroll
-      for (int j = 0; j < d; ++j) Crow[j] = 0.f;
-      if (r < d) {
-        ld(Crow, C + (tb * d + r) * d);
-        cr = c[tb * d + r];
-        gr = r < n ? dl_dx[tb * n + r] : dl_du[tb * m + (r - n)];
+        for (int i = 0; i < n; ++i) xt[i] = cur.x[i];
+#pragma unroll
+        for (int a = 0; a < m; ++a) ut[a] = cur.u[a];
+#pragma unroll
+        for (int j = 0; j < d; ++j) Crow[j] = cur.C[j];
+        cr = cur.c;
+        gr = cur.g;
       }
       float cdr = 0.f;
 #pragma unroll
@@ -373,13 +410,40 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
     for (int a = 0; a < m; ++a) au[a] = 0.f;
     if (r < kG) { I.dlam[r] = 0.f; I.lam[r] = 0.f; }
     __syncthreads();
+    // DILQR_IMPL_GPFD: step t-1's x, u, y and loss gradient loaded while step t computes
+    struct DIn {
+      float x[n], u[m], y[d], g;
+    };
+    auto load_d = [&](int t, DIn& in) {
+      const size_t tb = (size_t)t * B + b;
+      load_tau(tb, in.x, in.u);
+      const float* R0 = rec(t);
+#pragma unroll
+      for (int j = 0; j < d; ++j) in.y[j] = R0[W::Y + j];
+      in.g = 0.f;
+      if (r < d) in.g = r < n ? dl_dx[tb * n + r] : dl_du[tb * m + (r - n)];
+    };
+    DIn dnx;
+    if (DILQR_IMPL_GPFD && !(DILQR_IMPL_SKIP & 2)) load_d(T - 1, dnx);
     for (int t = (DILQR_IMPL_SKIP & 2) ? -1 : T - 1; t >= 0; --t) {
       const size_t tb = (size_t)t * B + b;
-      const float* R0 = rec(t);
       float xt[n], ut[m], y[d], Crow[d], cr = 0.f, gr = 0.f;
-      load_tau(tb, xt, ut);
+      {
+        DIn cur;
+        if (DILQR_IMPL_GPFD) {
+          cur = dnx;
+          if (t > 0) load_d(t - 1, dnx);
+        } else {
+          load_d(t, cur);
+        }
 #pragma unroll
-      for (int j = 0; j < d; ++j) { y[j] = R0[W::Y + j]; Crow[j] = 0.f; }
+        for (int i = 0; i < n; ++i) xt[i] = cur.x[i];
+#pragma unroll
+        for (int a = 0; a < m; ++a) ut[a] = cur.u[a];
+#pragma unroll
+        for (int j = 0; j < d; ++j) { y[j] = cur.y[j]; Crow[j] = 0.f; }
+        gr = cur.g;
+      }
       if (r < d) {
         if (crow_regs) {
 #pragma unroll
@@ -388,7 +452,6 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
           ld(Crow, C + (tb * d + r) * d);
         }
         cr = cv_regs ? cvr : c[tb * d + r];
-        gr = r < n ? dl_dx[tb * n + r] : dl_du[tb * m + (r - n)];
       }
       float tau[d];
 #pragma unroll
@@ -414,7 +477,12 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
       // row r of D_t -> LDS (t = T-1: only for the carry's D_u, F_{T-1} is zero)
       if (r < n) {
         float Fr[d];
+#if DILQR_IMPL_SKIP & 128                                  // timing only: no Jacobian in pass D
+#pragma unroll
+        for (int j = 0; j < d; ++j) Fr[j] = 0.f * xt[j % n];
+#else
         md.jac_row_sel(r, xt, ut, Fr);
+#endif
 #pragma unroll
         for (int j = 0; j < d; ++j) L.F[r][j] = Fr[j];
       }
@@ -441,8 +509,12 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
 #pragma unroll
         for (int j = 0; j < d; ++j) z += Mc[j] * y[j];
         if (r < d) {
+#if DILQR_IMPL_SKIP & 256                                  // timing only: no D^T dlam, D^T lam column sums
+          Dtd = I.dlam[r & 7]; Dtl = I.lam[r & 7];
+#else
 #pragma unroll
           for (int i = 0; i < n; ++i) { Dtd += L.F[i][r] * I.dlam[i]; Dtl += L.F[i][r] * I.lam[i]; }
+#endif
         }
         wr = gr - z;
         // dtheta_t = -(y^T Mp) + h_t^T gradx_t - dlam_{t+1}^T gradx_{t+1},
