@@ -28,6 +28,20 @@ namespace dilqr {
 // DILQR_G8_SKIP: timing-only builds (never the shipped library) that replace
 // the per-problem work every lane of a group repeats with stand-ins: bit 0 the
 // Jacobian, bit 1 the 3 x 3 gain solve (VERDICT r05 item 3's pricing)
+// DILQR_G8_PK (A/B builds; default 0): each lane's two rows (ra, rb) carried
+// as packed pairs through the step's products (bits: 1 V^T F, 2 F^T W, 4 the
+// value update, 8 C tau), so one v_pk_fma_f32 forms both rows' term with the
+// shared factor broadcast from one half; each half is the scalar fma chain of
+// the same terms in the same order (the same bits).  Measured at config 3
+// (profiles/r06/ab_rocket_sweep_g8_packed.txt): the value update alone (4)
+// 0.268-0.270 vs 0.267-0.268 ms per iteration, every other set slower
+// (0.288-0.339): the broadcast operands of the packed products need aligned
+// register pairs, and the unconstrained register-cost kernel leaves its
+// 128-VGPR budget (4 waves per SIMD) for AGPR copies and spills.
+#ifndef DILQR_G8_PK
+#define DILQR_G8_PK 0
+#endif
+#define G8PK_U ((DILQR_G8_PK & 5) != 0)
 #ifndef DILQR_G8_SKIP
 #define DILQR_G8_SKIP 0
 #endif
@@ -162,9 +176,15 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
   const int ra = l, rb = l + kG8;                  // ra < n in every lane; rb <= n (a V column or v) in lanes 0-5
   bool ok = true;                                  // iteration 0: this lane's rows diagonal and time-invariant
   float cd_last[2] = {0.f, 0.f}, cc_last[2] = {0.f, 0.f};
+#if G8PK_U
+  f2 U2[n];                                        // (column ra, column rb) of V_{t+1}, one pair per row
+#pragma unroll
+  for (int i = 0; i < n; ++i) U2[i] = f2{0.f, 0.f};
+#else
   float UA[n], UB[n];
 #pragma unroll
   for (int i = 0; i < n; ++i) { UA[i] = 0.f; UB[i] = 0.f; }
+#endif
   float prev_k[m];
 #pragma unroll
   for (int a = 0; a < m; ++a) prev_k[a] = 0.f;
@@ -194,9 +214,20 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
     for (int i = 0; i < n; ++i) tau[i] = xt[i];
 #pragma unroll
     for (int a = 0; a < m; ++a) tau[n + a] = ut[a];
+#if DILQR_G8_PK & 8
+    float Cta, Ctb;
+    {
+      f2 ct = f2{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < d; ++j) ct = ct + f2{CA[j], CB[j]} * tau[j];
+      Cta = ct.x;
+      Ctb = ct.y;
+    }
+#else
     float Cta = 0.f, Ctb = 0.f;
 #pragma unroll
     for (int j = 0; j < d; ++j) { Cta += CA[j] * tau[j]; Ctb += CB[j] * tau[j]; }
+#endif
     const float taua = ra < n ? x[tb * n + ra] : u[tb * m + (ra - n)];   // tau[ra], tau[rb]: loads, no select chains
     const float taub = rb < n ? x[tb * n + rb] : u[tb * m + (rb - n)];
     const float obj = group8_sum(0.5f * (taua * Cta) + taua * cra, 0.5f * (taub * Ctb) + taub * crb);
@@ -223,12 +254,29 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
         float Wa[d], Wb[d];
 #pragma unroll
         for (int j = 0; j < d; ++j) {
+#if DILQR_G8_PK & 1
+          f2 s2 = f2{0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < n; ++k)
+            if (FS::nz(k, j)) s2 = s2 + U2[k] * F[k][j];
+          Wa[j] = s2.x;
+          Wb[j] = s2.y;
+#else
           float sa = 0.f, sb = 0.f;
 #pragma unroll
           for (int k = 0; k < n; ++k)
-            if (FS::nz(k, j)) { sa += UA[k] * F[k][j]; sb += UB[k] * F[k][j]; }
+            if (FS::nz(k, j)) {
+#if G8PK_U
+              sa += U2[k].x * F[k][j];
+              sb += U2[k].y * F[k][j];
+#else
+              sa += UA[k] * F[k][j];
+              sb += UB[k] * F[k][j];
+#endif
+            }
           Wa[j] = sa;
           Wb[j] = sb;
+#endif
         }
 #pragma unroll
         for (int j = 0; j < d; ++j) L.Wt[ra][j] = Wa[j];
@@ -238,6 +286,23 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
         }
       }
       __syncthreads();
+#if DILQR_G8_PK & 2
+      f2 Wc2[n + 1];
+#pragma unroll
+      for (int k = 0; k <= n; ++k) Wc2[k] = f2{L.Wt[k][ra], L.Wt[k][rb]};
+#pragma unroll
+      for (int i = 0; i < d; ++i) {                // rows ra, rb of F^T V F
+        f2 s2 = f2{0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < n; ++k)
+          if (FS::nz(k, i)) s2 = s2 + F[k][i] * Wc2[k];
+        const f2 q2 = f2{CA[i], CB[i]} + s2;
+        QA[i] = q2.x;
+        QB[i] = q2.y;
+      }
+      qa = cba + Wc2[n].x;
+      qb = cbb + Wc2[n].y;
+#else
       float Wca[n + 1], Wcb[n + 1];
 #pragma unroll
       for (int k = 0; k <= n; ++k) { Wca[k] = L.Wt[k][ra]; Wcb[k] = L.Wt[k][rb]; }
@@ -252,6 +317,7 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
       }
       qa = cba + Wca[n];
       qb = cbb + Wcb[n];
+#endif
     }
     // Q overwrites W^T's words: every lane's W column reads above precede
     // these stores in the wave's program order (one wave per workgroup), and
@@ -324,6 +390,22 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
       }
 #pragma unroll
       for (int i = 0; i < n; ++i) {
+#if DILQR_G8_PK & 4
+        f2 s1 = f2{0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < m; ++a) s1 = s1 + L.Q[i][n + a] * f2{cola[a], colb[a]};
+        f2 v2 = f2{L.Q[i][cxa], L.Q[i][cxb]} + s1;
+        if constexpr (!SCHUR) {
+          f2 s2 = f2{0.f, 0.f}, s3 = f2{0.f, 0.f};
+#pragma unroll
+          for (int a = 0; a < m; ++a) {
+            s2 = s2 + Kall[a][i] * f2{Qna[a], Qnb[a]};
+            s3 = s3 + Kall[a][i] * f2{za[a], zb[a]};
+          }
+          v2 = (v2 + s2) + s3;
+        }
+        U2[i] = v2;
+#else
         float s1a = 0.f, s1b = 0.f;
 #pragma unroll
         for (int a = 0; a < m; ++a) {
@@ -344,8 +426,13 @@ DEV bool group8_sweep(LdsT& L, int T, int B, int b, int l, bool valid, const Mod
           va = (va + s2a) + s3a;
           vb = (vb + s2b) + s3b;
         }
+#if G8PK_U
+        U2[i] = f2{va, vb};
+#else
         UA[i] = va;
         UB[i] = vb;
+#endif
+#endif
       }
     }
     if (valid) {
