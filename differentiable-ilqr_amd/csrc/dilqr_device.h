@@ -197,6 +197,17 @@ template <int R, int Cc>
 DEV void ld2(float (&r)[R][Cc], const float* __restrict__ p) {
   ld<R * Cc>(*reinterpret_cast<float(*)[R * Cc]>(&r[0][0]), p);
 }
+// st with non-temporal stores (write-once outputs nothing in the kernel
+// reads back: the implicit backward's dC), K a multiple of 4
+typedef float f4 __attribute__((ext_vector_type(4)));
+template <int K>
+DEV void st_nt(float* __restrict__ p, const float (&r)[K]) {
+  static_assert(K % 4 == 0, "16-byte pieces");
+  f4* q = reinterpret_cast<f4*>(p);
+#pragma unroll
+  for (int i = 0; i < K / 4; ++i) __builtin_nontemporal_store(f4{r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]}, q + i);
+}
+
 template <int R, int Cc>
 DEV void st2(float* __restrict__ p, const float (&r)[R][Cc]) {
   st<R * Cc>(p, *reinterpret_cast<const float(*)[R * Cc]>(&r[0][0]));

@@ -29,6 +29,11 @@
 // DILQR_IMPL_GPFB / GPFD: passes B / D loading step t-1's inputs one step
 // ahead (A/B only: 1.16-1.25 ms with either, both or neither, within the
 // noise; profiles/r06/ab_implicit_rocket_prefetch_BD.txt)
+// DILQR_IMPL_NT: dC, dc written with non-temporal stores (A/B: ~2 % slower,
+// profiles/r06/ab_implicit_rocket_nt_stores.txt)
+#ifndef DILQR_IMPL_NT
+#define DILQR_IMPL_NT 0
+#endif
 #ifndef DILQR_IMPL_GPFB
 #define DILQR_IMPL_GPFB 0
 #endif
@@ -471,8 +476,13 @@ __global__ void __launch_bounds__(64, PASSES == 7   ? kGroupWavesPerSimd
         float dCr[d];
 #pragma unroll
         for (int j = 0; j < d; ++j) dCr[j] = -0.5f * (yr * tau[j] + taur * y[j]);
-        st(dC + (tb * d + r) * d, dCr);
-        dc[tb * d + r] = -yr;
+        if (DILQR_IMPL_NT) {
+          st_nt(dC + (tb * d + r) * d, dCr);
+          __builtin_nontemporal_store(-yr, dc + tb * d + r);
+        } else {
+          st(dC + (tb * d + r) * d, dCr);
+          dc[tb * d + r] = -yr;
+        }
       }
       // row r of D_t -> LDS (t = T-1: only for the carry's D_u, F_{T-1} is zero)
       if (r < n) {
