@@ -26,14 +26,14 @@
 #ifndef DILQR_IMPL_C_PF
 #define DILQR_IMPL_C_PF 1
 #endif
-// DILQR_IMPL_GPFB / GPFD: passes B / D loading step t-1's inputs one step
-// ahead (A/B only: 1.16-1.25 ms with either, both or neither, within the
-// noise; profiles/r06/ab_implicit_rocket_prefetch_BD.txt)
 // DILQR_IMPL_NT: dC, dc written with non-temporal stores (A/B: ~2 % slower,
 // profiles/r06/ab_implicit_rocket_nt_stores.txt)
 #ifndef DILQR_IMPL_NT
 #define DILQR_IMPL_NT 0
 #endif
+// DILQR_IMPL_GPFB / GPFD: passes B / D loading step t-1's inputs one step
+// ahead (A/B only: 1.16-1.25 ms with either, both or neither, within the
+// noise; profiles/r06/ab_implicit_rocket_prefetch_BD.txt)
 #ifndef DILQR_IMPL_GPFB
 #define DILQR_IMPL_GPFB 0
 #endif
