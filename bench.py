@@ -637,8 +637,12 @@ def profile_set(name, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # defaults: 200 warmup solves (~75 ms) before the timed ones.  The GPU's
+    # clocks ramp over tens of milliseconds of load; 5 warmup solves (1.9 ms)
+    # timed a cold GPU: 1.70-1.72e9 against 1.87-1.88e9 once warm, on one box
+    # (profiles/r06/bench_warmup_sweep.txt)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--lqr-iter", type=int, default=10)
     ap.add_argument("--batch", type=int, default=B_PER_GPU, help="problems per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -707,13 +711,20 @@ def main():
     if dist:
         tdist.barrier()
     torch.cuda.synchronize(dev)
+    # HIP events on the launch stream bracket the same K solves: the roofline's
+    # per-launch duration of the dominant kernel is measured over the timed
+    # region itself (one step = k_mpc_solve_fixed + k_mpc_fixed_finish)
+    ev_t0, ev_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev_t0.record(stream)
     for _ in range(args.steps):
         step()
+    ev_t1.record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
+    timed_solve_ms = ev_t0.elapsed_time(ev_t1) / args.steps if args.steps else None
     ranks = None
     if dist:
         own = elapsed
@@ -737,7 +748,10 @@ def main():
     # step), reps solves back to back between one pair of HIP events on ITS
     # stream (the current stream, where ops launch it)
     reps = 10
-    solve_ms = _event_ms(stream, lambda r: step(), reps)
+    # the same solves back to back after a ~5-ms stream sleep (one busy wave:
+    # the clocks fall back meanwhile) — reported beside the timed-region figure
+    solve_ms_after_idle = _event_ms(stream, lambda r: step(), reps)
+    solve_ms = timed_solve_ms if timed_solve_ms is not None else solve_ms_after_idle
     solve_bytes = float(solve_bytes_per_problem(sv.cost_sym.cpu().numpy(), args.lqr_iter).sum())
     # ---- the per-iteration kernel of the stop-rule path (k_mpc_iterate<...,
     # FIRST=false>): iterations 1..reps of a solve launched back to back.  No
@@ -816,6 +830,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_measured_at": head_pmc.get("measured_at", PMC_COMMIT[0]),
                          "algorithmic_bytes_per_launch": solve_bytes, "avg_launch_ms": solve_ms,
+                         "avg_launch_ms_source": "HIP events on the launch stream around the timed solves",
+                         "avg_launch_ms_after_idle": solve_ms_after_idle,
                          "limiter": {"what": "VALU issue at one wave per SIMD (B=65536 = 1024 waves); not HBM",
                                      **{k: v for k, v in head_pmc.items()
                                         if k not in ("hbm_bytes_per_launch", "measured_at")}},

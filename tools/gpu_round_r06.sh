@@ -29,7 +29,7 @@ if has prof; then
   R=$(pwd)
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof -o run --output-format csv -- \
-      python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $R/$OUT/prof.log 2>&1; rc=$?
+      python3 $R/bench.py --no-cpu-baseline > $R/$OUT/prof.log 2>&1; rc=$?
   echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_k -o run --output-format csv -- \
       python3 $R/bench.py --kernels-only > $R/$OUT/prof_k.log 2>&1; rc=$?
