@@ -166,16 +166,33 @@ def _timed_solves(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, lqr_iter
     return sv.B * lqr_iter * solves / dt, dt * 1e3 / (lqr_iter * solves)
 
 
-def _event_ms(stream, fn, reps):
+def _event_ms(stream, fn, reps, warm_ms=20.0, prep=None):
     """Average time of fn(r), r = 0..reps-1, launched back to back between ONE
     pair of HIP events on `stream` (an event pair around every launch adds
     several us of its own to a 40-us kernel; rocprof's kernel durations agree
-    with this figure, profiles/)."""
+    with this figure, profiles/).  A stateful fn (an MPC iteration) passes
+    `prep`, which re-establishes its starting state (begin + iteration 0, launches
+    only) after the warm-up calls, so the timed calls see the states they would
+    have seen without them."""
+    # first call alone: its duration sizes the warm-up below
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    fn(0)
+    torch.cuda.synchronize()
+    est_ms = (time.perf_counter() - t) * 1e3
+    warm = int(min(400, max(2, warm_ms / max(est_ms, 1e-3))))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # the stream sleeps (~5 ms) while the host queues every launch, so the event
-    # pair times the kernels back to back, not the host's launch rate (a ctypes
-    # launch takes tens of us of Python, comparable to one 36-us iteration)
-    torch.cuda._sleep(10_000_000)
+    # the stream sleeps while the host queues every launch, so the event pair
+    # times the kernels back to back, not the host's launch rate (a ctypes
+    # launch takes tens of us of Python, comparable to one 36-us iteration);
+    # then ~warm_ms of untimed calls before the first event, since the clocks
+    # fall back while one wave spins and ramp again over tens of ms of load
+    # (profiles/r06/bench_warmup_sweep.txt)
+    torch.cuda._sleep(int(min(100.0, 2.0 + 0.05 * (warm + reps)) * 2e6))
+    for r in range(warm):
+        fn(r % max(reps, 1))
+    if prep is not None:
+        prep()
     e0.record(stream)
     for r in range(reps):
         fn(r)
@@ -238,11 +255,13 @@ def dense_cost_roofline(dev, x0, theta, B, reps=10):
     nb, _ = N.make_bounds(None, None)
     s = N.stream(dev)
     stream = torch.cuda.current_stream(dev)
-    sv.begin(N.MODEL_CARTPOLE, theta, x0)
-    sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
+    def prep():
+        sv.begin(N.MODEL_CARTPOLE, theta, x0)
+        sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, nb, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
+    prep()
     ms = _event_ms(stream, lambda r: N.call("dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T, B, N.ptr(theta), N.ptr(x0),
                                             N.ptr(C), N.ptr(c), nb, 0.5, 2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s),
-                   reps)
+                   reps, prep=prep)
     cf = iter_cost_floats(sv.cost_sym.cpu().numpy())
     nbytes = float(iter_bytes_per_problem(cf).sum())
     gbs = nbytes / (ms * 1e-3) / 1e9
@@ -408,11 +427,14 @@ def steady_iteration_ms(sv, model_id, theta, x0, C, c, bounds, decay, max_ls, de
     not_improved_lim = inf) between one pair of HIP events on the launch stream."""
     from dilqr import _native as N
     s = N.stream(dev)
-    sv.begin(model_id, theta, x0)
-    sv.iterate(model_id, theta, x0, C, c, bounds, decay, max_ls, 0, 1e-4, 0.0, 10 ** 9)
+
+    def prep():
+        sv.begin(model_id, theta, x0)
+        sv.iterate(model_id, theta, x0, C, c, bounds, decay, max_ls, 0, 1e-4, 0.0, 10 ** 9)
+    prep()
     return _event_ms(torch.cuda.current_stream(dev), lambda r: N.call(
         "dilqr_mpc_step_f32", model_id, sv.T, sv.B, N.ptr(theta), N.ptr(x0), N.ptr(C), N.ptr(c), bounds,
-        float(decay), int(max_ls), r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s), reps)
+        float(decay), int(max_ls), r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s), reps, prep=prep)
 
 
 def secondary_configs(dev):
@@ -748,20 +770,22 @@ def main():
     # step), reps solves back to back between one pair of HIP events on ITS
     # stream (the current stream, where ops launch it)
     reps = 10
-    # the same solves back to back after a ~5-ms stream sleep (one busy wave:
-    # the clocks fall back meanwhile) — reported beside the timed-region figure
-    solve_ms_after_idle = _event_ms(stream, lambda r: step(), reps)
-    solve_ms = timed_solve_ms if timed_solve_ms is not None else solve_ms_after_idle
+    # the same solves timed again by the secondary lines' event helper (a
+    # cross-check of the timed-region figure)
+    solve_ms_separate = _event_ms(stream, lambda r: step(), reps)
+    solve_ms = timed_solve_ms if timed_solve_ms is not None else solve_ms_separate
     solve_bytes = float(solve_bytes_per_problem(sv.cost_sym.cpu().numpy(), args.lqr_iter).sum())
     # ---- the per-iteration kernel of the stop-rule path (k_mpc_iterate<...,
     # FIRST=false>): iterations 1..reps of a solve launched back to back.  No
     # stop-rule launches in between: with eps = 0 and not_improved_lim = inf the
     # rule cannot fire.
-    sv.begin(N.MODEL_CARTPOLE, theta, x0)
-    sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
+    def prep_iter():
+        sv.begin(N.MODEL_CARTPOLE, theta, x0)
+        sv.iterate(N.MODEL_CARTPOLE, theta, x0, C, c, bounds, 0.5, 2, 0, 1e-4, 0.0, 10 ** 9)
+    prep_iter()
     iter_ms = _event_ms(stream, lambda r: N.call(
         "dilqr_mpc_step_f32", N.MODEL_CARTPOLE, T_HORIZON, B, N.ptr(theta), N.ptr(x0), N.ptr(C), N.ptr(c), bounds,
-        0.5, 2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s), reps)
+        0.5, 2, r + 1, 1e-4, 0.0, 10 ** 9, sv.state, s), reps, prep=prep_iter)
     cost_floats = iter_cost_floats(sv.cost_sym.cpu().numpy())
     iter_bytes = float(iter_bytes_per_problem(cost_floats).sum())
     cost_path = ("time-invariant diagonal cost held in registers (2d floats per problem)"
@@ -831,7 +855,7 @@ def main():
                          "traffic_measured_at": head_pmc.get("measured_at", PMC_COMMIT[0]),
                          "algorithmic_bytes_per_launch": solve_bytes, "avg_launch_ms": solve_ms,
                          "avg_launch_ms_source": "HIP events on the launch stream around the timed solves",
-                         "avg_launch_ms_after_idle": solve_ms_after_idle,
+                         "avg_launch_ms_separate": solve_ms_separate,
                          "limiter": {"what": "VALU issue at one wave per SIMD (B=65536 = 1024 waves); not HBM",
                                      **{k: v for k, v in head_pmc.items()
                                         if k not in ("hbm_bytes_per_launch", "measured_at")}},
