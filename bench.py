@@ -190,6 +190,8 @@ def _event_ms(stream, fn, reps, warm_ms=20.0, prep=None):
     # (profiles/r06/bench_warmup_sweep.txt)
     torch.cuda._sleep(int(min(100.0, 2.0 + 0.05 * (warm + reps)) * 2e6))
     for r in range(warm):
+        if prep is not None and r % max(reps, 1) == 0:
+            prep()                  # warm calls repeat the timed sequence (iterations 1..reps)
         fn(r % max(reps, 1))
     if prep is not None:
         prep()
