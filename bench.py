@@ -500,7 +500,7 @@ def secondary_configs(dev):
     ms = implicit_kernel_ms(dx, wx, wu, C, c, x, u, K, None, None, dev)
     out["config3_rocket"]["implicit_backward"] = implicit_roofline(
         "k_implicit_backward_group<Rocket> (dC, dc, dtheta)", implicit_flops_per_problem("rocket", T) * B,
-        implicit_boundary_bytes(n, m, T, B), ms, B, T, "none", "k_implicit_backward_group<Rocket, RocketD2, 0>")
+        implicit_boundary_bytes(n, m, T, B), ms, B, T, "none", "k_implicit_backward_group<Rocket, RocketD2, 0, 7>")
     del sv, C, c, x0, x, u, F, K, wx, wu
     # ---- config 4: cartpole T=25 B=65536 with bounds (+-100 reference value, +-10 stress) + implicit backward
     T, B, n, m = 25, 65536, 5, 1
