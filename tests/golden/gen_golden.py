@@ -334,6 +334,25 @@ def run_mpc(name, dt, lqr_iter_override=None):
     return x0, np_(x), np_(u), np_(costs)
 
 
+MPC_ITERATE_CASES = ("cart_unc", "cart_box10", "pend_box")   # per-iteration goldens (lqr_iter 1, 2, 3)
+
+
+def case_mpc_iterates():
+    """Only the per-iteration entries of MPC_ITERATE_CASES, merged into the
+    existing mpc_{f64,f32}.npz (the rest of those files is left as it is)."""
+    print("E'. mpc per-iteration entries")
+    for dt in (torch.float64, torch.float32):
+        with default_dtype(dt):
+            path = os.path.join(OUT, f"mpc_{tname(dt)}.npz")
+            with np.load(path) as old:
+                out = {k: old[k] for k in old.files}
+            for name in MPC_ITERATE_CASES:
+                for k in (1, 2, 3):
+                    _, x, u, costs = run_mpc(name, dt, lqr_iter_override=k)
+                    out.update({f"{name}_it{k}_x": x, f"{name}_it{k}_u": u, f"{name}_it{k}_costs": costs})
+            save(f"mpc_{tname(dt)}", **out)
+
+
 def case_mpc():
     print("E. mpc")
     for dt in (torch.float64, torch.float32):
@@ -342,7 +361,7 @@ def case_mpc():
             for name in MPC_CASES:
                 x0, x, u, costs = run_mpc(name, dt)
                 out.update({f"{name}_x0": x0, f"{name}_x": x, f"{name}_u": u, f"{name}_costs": costs})
-                if name in ("cart_unc", "cart_box10"):
+                if name in MPC_ITERATE_CASES:
                     for k in (1, 2, 3):
                         _, x, u, costs = run_mpc(name, dt, lqr_iter_override=k)
                         out.update({f"{name}_it{k}_x": x, f"{name}_it{k}_u": u, f"{name}_it{k}_costs": costs})
@@ -866,7 +885,8 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["models", "riccati", "pnqp", "lqrstep", "mpc", "adjoint", "implicit",
                              "implicit25", "datasets", "il", "generic", "api", "complex", "stepgen"]
     table = {"models": case_models, "riccati": case_riccati, "pnqp": case_pnqp,
-             "lqrstep": case_lqrstep, "mpc": case_mpc, "adjoint": case_classic_adjoint,
+             "lqrstep": case_lqrstep, "mpc": case_mpc, "mpc_iterates": case_mpc_iterates,
+             "adjoint": case_classic_adjoint,
              "implicit": case_implicit, "implicit25": case_implicit25, "datasets": case_datasets, "il": case_il,
              "generic": case_generic, "api": case_api, "complex": case_complex, "stepgen": case_stepgen}
     for w in which:

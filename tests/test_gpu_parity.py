@@ -333,6 +333,25 @@ def test_mpc_solve_vs_oracle(golden, name):
     assert np.all(rerr < np.maximum(1e-4, 3 * spread)), (np.flatnonzero(rerr >= 1e-4), rerr.max())
 
 
+@pytest.mark.parametrize("k", [1, 2, 3])
+@pytest.mark.parametrize("name", ["cart_unc", "cart_box10", "pend_box"])
+def test_mpc_iterates_vs_golden(golden, name, k):
+    """The solve stopped after k = 1, 2, 3 iterations (lqr_iter = k) against the
+    reference's own fp64 solves with the same lqr_iter (gen_golden.py
+    MPC_ITERATE_CASES): the per-iteration path of mpc_explicit.py:228-299, not
+    only its end point.  Costs within max(1e-4, 3x the reference's own
+    fp32-vs-fp64 spread) relative, as test_mpc_solve_vs_oracle."""
+    g = golden("mpc_f64")
+    mname, T, it, bounds, eps, nil, decay, mls = MPC_CASES[name]
+    x0 = g[f"{name}_x0"]
+    _, _, costs = run_gpu_mpc(x0, mname, T, k, bounds, eps, nil, decay, mls)
+    ref = g[f"{name}_it{k}_costs"]
+    spread = np.abs(golden("mpc_f32")[f"{name}_it{k}_costs"] - ref) / np.maximum(1.0, np.abs(ref))
+    rerr = np.abs(cpu(costs) - ref) / np.maximum(1.0, np.abs(ref))
+    print(f"[{name} k={k}] max rel {rerr.max():.2e}, reference fp32 spread max {spread.max():.2e}")
+    assert np.all(rerr < np.maximum(1e-4, 3 * spread)), (np.flatnonzero(rerr >= 1e-4), rerr.max())
+
+
 COMPLEX_MPC = {"fixed": (20, 10, 0.0, 10 ** 9), "il": (20, 40, 1e-3, 5)}     # T, lqr_iter, eps, not_improved_lim
 
 
