@@ -280,12 +280,15 @@ struct FwdIn {
   }
 };
 
-// Prefetch distance of the fused sweep and line search, in steps.  At B =
-// 65536 the one-problem-per-lane kernels run ONE wave per SIMD, so the only
-// latency cover is the loads already in flight.  Two steps ahead measured no
-// faster than one (0.0702 vs 0.0695 ms per iteration, config 2), so 1.
+// Prefetch distance of the fused sweep, in steps.  At B = 65536 the
+// one-problem-per-lane kernels run ONE wave per SIMD, so the only latency
+// cover is the loads already in flight.  Round 2 measured two steps ahead no
+// faster than one (0.0702 vs 0.0695 ms per iteration, config 2) — on a GPU
+// short of its clocks (bench's 5 warmup solves); warm, round 6: the headline
+// 1.873-1.877e9 -> 1.917-1.923e9, the steady iteration 34.0 -> 33.5 us
+// (profiles/r06/ab_sweep_prefetch2.txt), so 2.
 #ifndef DILQR_PF
-#define DILQR_PF 1
+#define DILQR_PF 2
 #endif
 constexpr int kPF = DILQR_PF;
 // The line search's: 2 was faster with SLP vectorisation on (round 2); in
