@@ -293,12 +293,14 @@ struct FwdIn {
 constexpr int kPF = DILQR_PF;
 // The line search's: 2 was faster with SLP vectorisation on (round 2); in
 // the no-SLP build 1 is (headline A/B, 4 rounds on one box: 1.742e9 ->
-// 1.772e9 problem-iterations/s — one buffer copy per step instead of two).
+// 1.772e9 problem-iterations/s — one buffer copy per step instead of two);
+// re-measured warm in round 6 (with the sweep at 2): 1.920e9 at 1 against
+// 1.853e9 at 2 (profiles/r06/ab_ls_prefetch2.txt).
 #ifndef DILQR_PF_LS
 #define DILQR_PF_LS 1
 #endif
 constexpr int kPFL = DILQR_PF_LS;                   // the line search's prefetch distance
-static_assert(kPFL == 1, "the line search prefetches one step ahead");
+static_assert(kPFL == 1 || kPFL == 2, "the line search prefetches one or two steps ahead");
 
 #ifndef DILQR_PHASE_SKIP
 #define DILQR_PHASE_SKIP 0
@@ -365,11 +367,14 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
     f2 cp = {0.f, 0.f};
     // step s's record holds x_{s+1} of the current trajectory; indices clamp at T-1
     auto cl = [T](int s) { return s < T ? s : T - 1; };
-    FwdIn<n, m, GREC, TL, BM> cur, n1;
+    FwdIn<n, m, GREC, TL, BM> cur, n1, n2;
     cur.load(ws, u, cs, x, bd, T, 0, cl(1), B, b);
     if constexpr (TL == TRAJ_REC) {                     // u_0 from record 0
       float x0r[n];
       ld_xu<TL>(x0r, cur.u, x, u, 0, B, b);
+    }
+    if constexpr (kPFL >= 2) {
+      if (T > 1) n1.load(ws, u, cs, x, bd, T, 1, cl(2), B, b);
     }
     // step T-1 is peeled off the loop (LAST: no prefetch, no dynamics step), so
     // the loop body updates the candidate states unconditionally — no branch
@@ -377,7 +382,13 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
     // c: this step's inputs, nx: the next step's, loaded here (prefetch 1)
     auto step = [&](int t, auto last_c, auto& c, auto& nx) {
       constexpr bool LAST = decltype(last_c)::value;
-      if constexpr (!LAST) nx.load(ws, u, cs, x, bd, T, t + 1, cl(t + 2), B, b);      // prefetch step t+1
+      if constexpr (!LAST) {
+        if constexpr (kPFL >= 2) {
+          if (t + 2 < T) n2.load(ws, u, cs, x, bd, T, t + 2, cl(t + 3), B, b);    // prefetch step t+2
+        } else {
+          nx.load(ws, u, cs, x, bd, T, t + 1, cl(t + 2), B, b);                   // prefetch step t+1
+        }
+      }
       f2 nu[m];
 #pragma unroll
       for (int a = 0; a < m; ++a) {
@@ -455,6 +466,7 @@ DEV int line_search(int T, int B, int b, const Model md, const float* __restrict
     for (int t = 0; t < T - 1; ++t) {
       step(t, std::false_type{}, cur, n1);
       cur = n1;
+      if constexpr (kPFL >= 2) n1 = n2;
     }
     step(T - 1, std::true_type{}, cur, n1);
     const float cA = cp.x, cB = cp.y;
